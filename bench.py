@@ -1,0 +1,252 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X block-circulant (BC) linear forward — BASELINE.json's metric.
+
+Workload (north star / metric): one BlockCirculantLinear forward, 4096 -> 4096, b = 128,
+N = batch*seq = 8192 tokens per GPU, fp32 I/O (the reference's fp32 path), weight spectra
+precomputed outside the timed region (the reference's cache_cfft=1 perf convention,
+bench_all_in_one.py:484). A "step" = one forward over the rank's 8192-token shard.
+
+Multi-GPU: one process per GPU (torch.distributed.run); tokens are sharded, each rank runs
+its own 8192-token shard (weak scaling) with no collective in the data path. With
+--allgather the single RCCL all-gather of the output shards (north star) is timed in a
+second loop and reported as `with_allgather`.
+
+Prints ONE JSON line on rank 0. `roofline.achieved` = algorithmic bytes per launch
+(N*K*s_x + N*M*s_y + nO*nI*(b/2+1)*8 [+ M*s_bias]) / the kernel's average
+duration measured with HIP events on the launch stream. `roofline.traffic` = HBM bytes per
+launch from rocprofv3 PMC counters (profiles/pmc_traffic_*.json, written by
+tools/pmc_traffic.py) or null. `cpu_baseline` times the oracle's torch-CPU restatement
+(oracle/bc_oracle.py) on a bounded token sample on the host cores.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "llama-fft_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+FP32_VALU_TFLOPS = 157.3     # beside it: the FP32 vector ceiling (intensity straddles the ridge)
+METRIC = "BC-linear GTok-elem/s + GB/s vs roofline, b=128 4096→4096, 1/2/4/8 GPU"
+DT = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}
+SZ = {"fp32": 4, "bf16": 2, "fp16": 2}
+
+
+def algo_bytes(n, k, m, b, io, bias):
+    n_out, n_in = m // b, k // b
+    return n * k * SZ[io] + n * m * SZ[io] + n_out * n_in * (b // 2 + 1) * 8 + (m * SZ[io] if bias else 0)
+
+
+def algo_flops(n, k, m, b):
+    import math
+    n_out, n_in = m // b, k // b
+    return n * (8 * n_out * n_in * (b // 2 + 1) + (n_in + n_out) * 2.5 * b * math.log2(b))
+
+
+def make_layer(k, m, b, io, bias, dev, seed=1):
+    from patch_llama_fft import BlockCirculantLinear
+    torch.manual_seed(seed)                                   # c ~ 0.01 N(0,1), seed 1 (§8d)
+    layer = BlockCirculantLinear(k, m, block_size=b, bias=bias)
+    if bias:
+        with torch.no_grad():
+            layer.bias.normal_(0.0, 0.1)
+    return layer.to(dev).to(DT[io]).eval()
+
+
+def time_layer(layer, x, steps, warmup, barrier=None):
+    """Returns (wall ms per step over the bracketed region, mean kernel ms from events)."""
+    stream = torch.cuda.current_stream()
+    with torch.inference_mode():
+        layer._spectra(layer.c)                                # spectra outside timing
+        for _ in range(warmup):
+            layer(x)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        if barrier:
+            barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for s, e in ev:
+            s.record(stream)
+            layer(x)
+            e.record(stream)
+        torch.cuda.synchronize()
+        if barrier:
+            barrier()
+        wall = (time.perf_counter() - t0) * 1e3 / steps
+    kern = sum(s.elapsed_time(e) for s, e in ev) / steps
+    return wall, kern
+
+
+def load_traffic(tag):
+    """Per-launch HBM bytes from the newest profiles/pmc_traffic_*.json for this workload."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic_*.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if tag in d:
+            return d[tag].get("hbm_bytes_per_launch")
+    return None
+
+
+def cpu_baseline(k, m, b, io, bias, budget_s):
+    """Oracle's torch-CPU restatement of the cached forward (bench_all_in_one.py:179-231),
+    fp32, on a bounded token sample; GTok-elem/s."""
+    sys.path.insert(0, ROOT)
+    from oracle.bc_oracle import torch_cpu_forward_cached
+    threads = int(os.environ.get("BENCH_CPU_THREADS", min(os.cpu_count() or 1, 16)))
+    torch.set_num_threads(threads)
+    n = 1024
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(n, k, generator=g)
+    c = torch.randn(m // b, k // b, b, generator=g) * 0.01
+    cf = torch.fft.rfft(c, dim=-1)
+    bv = torch.randn(m, generator=g) * 0.1 if bias else None
+    torch_cpu_forward_cached(x, cf, bv, b)                     # warmup
+    it, t0 = 0, time.perf_counter()
+    while True:
+        torch_cpu_forward_cached(x, cf, bv, b)
+        it += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or it >= 10000:
+            break
+    return {"value": round(n * m * it / el / 1e9, 5), "unit": "GTok-elem/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{it} x forward of {n} tokens, {k}->{m} b={b} fp32 (torch CPU rfft/einsum/"
+                      f"irfft, cached spectra), {el:.1f} s on {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--tokens", type=int, default=8192, help="tokens per rank (batch*seq)")
+    ap.add_argument("--in-features", type=int, default=4096)
+    ap.add_argument("--out-features", type=int, default=4096)
+    ap.add_argument("--block-size", type=int, default=128)
+    ap.add_argument("--io", default="fp32", choices=list(DT))
+    ap.add_argument("--bias", type=int, default=0)
+    ap.add_argument("--allgather", type=int, default=1, help="also time the RCCL all-gather (N>1)")
+    ap.add_argument("--variants", type=int, default=1, help="also time bf16-I/O and config-2 shapes")
+    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU baseline work")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+        barrier = lambda: dist.barrier(device_ids=[local])  # noqa: E731
+    else:
+        barrier = None
+
+    n, k, m, b, io = args.tokens, args.in_features, args.out_features, args.block_size, args.io
+    layer = make_layer(k, m, b, io, bool(args.bias), dev)
+    torch.manual_seed(1000 + rank)                           # x ~ N(0,1) per rank shard
+    x = torch.randn(n, k, device=dev).to(DT[io])
+
+    wall, kern = time_layer(layer, x, args.steps, args.warmup, barrier)
+    t = torch.tensor([wall, kern], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall, kern = float(t[0]), float(t[1])
+
+    nbytes = algo_bytes(n, k, m, b, io, bool(args.bias))
+    gbs = nbytes / (kern * 1e-3) / 1e9
+    total_elems = n * m * world
+    value = total_elems / (wall * 1e-3) / 1e9
+
+    gather = None
+    if world > 1 and args.allgather:
+        with torch.inference_mode():
+            y = layer(x)
+            out = torch.empty((world * n, m), dtype=y.dtype, device=dev)
+            for _ in range(3):
+                dist.all_gather_into_tensor(out, layer(x))
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                dist.all_gather_into_tensor(out, layer(x))
+            torch.cuda.synchronize()
+            barrier()
+            g_ms = (time.perf_counter() - t0) * 1e3 / args.steps
+        tg = torch.tensor([g_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(tg, op=dist.ReduceOp.MAX)
+        gather = {"ms_per_step": round(float(tg[0]), 4),
+                  "value": round(total_elems / (float(tg[0]) * 1e-3) / 1e9, 3),
+                  "note": "forward + RCCL all_gather_into_tensor of all y shards to every rank"}
+
+    variants = []
+    if args.variants and rank == 0 and world == 1:
+        for (vk, vm, vb, vio, vn) in [(4096, 4096, 128, "bf16", 8192), (4096, 11008, 128, "bf16", 8192),
+                                      (4096, 4096, 64, "fp32", 8192), (4096, 4096, 256, "fp32", 8192)]:
+            vl = make_layer(vk, vm, vb, vio, False, dev)
+            vx = torch.randn(vn, vk, device=dev).to(DT[vio])
+            vw, vkern = time_layer(vl, vx, max(10, args.steps // 2), 5)
+            vbytes = algo_bytes(vn, vk, vm, vb, vio, False)
+            variants.append({"workload": f"{vk}->{vm} b={vb} N={vn} {vio}-io",
+                             "ms": round(vkern, 4),
+                             "GTok_elem_s": round(vn * vm / (vkern * 1e-3) / 1e9, 3),
+                             "GB_s": round(vbytes / (vkern * 1e-3) / 1e9, 1),
+                             "frac": round(vbytes / (vkern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+            del vl, vx
+
+    tag = f"{k}x{m}_b{b}_n{n}_{io}"
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_budget > 0:
+        cpu = cpu_baseline(k, m, b, io, bool(args.bias), args.cpu_budget)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 4),
+            "unit": "GTok-elem/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (x~N(0,1) seed 1000+rank, c~0.01 N(0,1) seed 1)",
+            "config": {"workload": f"BlockCirculantLinear.forward {k}->{m} b={b}, {n} tokens/rank, "
+                                   f"{io} I/O, spectra cached",
+                       "in_features": k, "out_features": m, "block_size": b,
+                       "tokens_per_rank": n, "global_tokens": n * world, "io_dtype": io,
+                       "bias": bool(args.bias), "parallelism": f"token-shard x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                         "traffic": load_traffic(tag),
+                         "kernel": "bc_forward_kernel", "kernel_ms": round(kern, 5),
+                         "algorithmic_bytes_per_launch": nbytes,
+                         "fp32_tflops": round(algo_flops(n, k, m, b) / (kern * 1e-3) / 1e12, 2),
+                         "fp32_valu_peak_tflops": FP32_VALU_TFLOPS},
+            "cpu_baseline": cpu,
+        }
+        if gather:
+            line["with_allgather"] = gather
+        if variants:
+            line["variants"] = variants
+        print(json.dumps(line), flush=True)
+
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,90 @@
+/*
+ * bcfft.h — C ABI of the MI355X block-circulant (BC) linear engine (libbcfft.so).
+ *
+ * This is the drop-in boundary BELOW the reference's Python module API. The reference
+ * (Pinguhat/llama-fft) has no FFI of its own: every entry point here replaces a torch call
+ * sequence inside its module, cited per function (paths relative to the reference's src/).
+ * The Python mirror of the module API (llama-fft_amd/patch_llama_fft.py) binds these with
+ * ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; every buffer is caller-owned device memory (torch's
+ *    allocator in the Python layer). No entry point allocates, frees or synchronises.
+ *  - `stream` is a hipStream_t passed as void* (NULL = legacy default stream). Work is
+ *    enqueued asynchronously; entry points are reentrant and keep no mutable global state.
+ *  - Return value: BCFFT_OK (0) or a BCFFT_ERR_* status. Shape/dtype/alignment problems are
+ *    reported before anything is launched. bcfft_status_string() gives a message.
+ *  - dtype codes: BCFFT_F32, BCFFT_F16, BCFFT_BF16 (BCFFT_NONE for "no bias").
+ *  - Block sizes: 32, 64, 128, 256 (power-of-two b with the 4- or 8-lane four-step FFT).
+ */
+#ifndef BCFFT_H
+#define BCFFT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BCFFT_ABI_VERSION 1
+
+enum bcfft_dtype { BCFFT_NONE = -1, BCFFT_F32 = 0, BCFFT_F16 = 1, BCFFT_BF16 = 2 };
+
+enum bcfft_status {
+  BCFFT_OK = 0,
+  BCFFT_ERR_SHAPE = 1,   /* features not divisible by block_size, non-positive sizes      */
+  BCFFT_ERR_BLOCK = 2,   /* unsupported block_size                                          */
+  BCFFT_ERR_DTYPE = 3,   /* unsupported dtype code / output dtype != promote(x, bias)       */
+  BCFFT_ERR_ALIGN = 4,   /* x / y / spectra not 16-byte aligned                              */
+  BCFFT_ERR_HIP = 5,     /* a HIP launch failed (bcfft_last_hip_error() has the text)        */
+  BCFFT_ERR_ARG = 6      /* NULL pointer where one is required                               */
+};
+
+/* ABI version of the loaded library (== BCFFT_ABI_VERSION it was built with). */
+int bcfft_abi_version(void);
+
+/* Human-readable text for a status code. */
+const char* bcfft_status_string(int status);
+
+/* Text of the last HIP error seen by this thread (empty if none). */
+const char* bcfft_last_hip_error(void);
+
+/* Bytes of the packed spectra buffer for an (n_out_blocks x n_in_blocks) grid of b x b
+ * circulant blocks: n_out*n_in*(b/2) complex64 packed bins + a b-entry twiddle table. */
+int64_t bcfft_spectra_bytes(int n_out_blocks, int n_in_blocks, int block_size);
+
+/* Packed weight spectra. Replaces `Cf = torch.fft.rfft(self.c.to(float32), dim=-1)`
+ * (patch_llama_fft.py:256-257) and the memoised Cf of the cached forward
+ * (bench_all_in_one.py:204-216).
+ *   c:        (n_out_blocks, n_in_blocks, block_size) contiguous, dtype c_dtype
+ *   spectra:  bcfft_spectra_bytes(...) bytes, 16-B aligned; receives
+ *             S[o][i][k] = rfft(c[o,i])[k] / (2b) for 0<k<b/2, S[o][i][0] = (X0, X_{b/2})/(2b)
+ *   transpose_conj = 1 writes the adjoint layout S[i][o][k] = conj(...) instead (the
+ *             spectra of the transposed operator, used for dL/dx in the backward pass).
+ * Computed in fp64 and rounded once to fp32. */
+int bcfft_spectra(const void* c, int c_dtype, int n_out_blocks, int n_in_blocks, int block_size,
+                  int transpose_conj, void* spectra, void* stream);
+
+/* Fused BC forward. Replaces BlockCirculantLinear.forward's body
+ * (patch_llama_fft.py:246-271: reshape, .to(fp32), rfft, einsum "oif,nif->nof", irfft,
+ * .to(x.dtype), + bias) with ONE kernel launch.
+ *   x:  (n_tokens, in_features) row-major, dtype x_dtype, 16-B aligned
+ *   y:  (n_tokens, out_features) row-major, y_dtype == promote(x_dtype, bias_dtype)
+ *   bias: (out_features,) of bias_dtype, or NULL with bias_dtype = BCFFT_NONE
+ * Numerics follow the reference: fp32 spectra math, result rounded to x_dtype, then the
+ * bias added in fp32 and the sum rounded to y_dtype. n_tokens == 0 is a no-op. */
+int bcfft_forward(const void* x, int x_dtype, int64_t n_tokens, int in_features,
+                  int out_features, int block_size, const void* spectra, const void* bias,
+                  int bias_dtype, void* y, int y_dtype, void* stream);
+
+/* Single circulant matvec y = C(c) x, C[i,j] = c[(i-j) mod n], any n >= 1.
+ * Replaces fft_utils.circulant_matvec_fft (fft_utils.py:3-34); c, x, y share `dtype`.
+ * Direct O(n^2) evaluation accumulated in fp64 (this entry point serves validation-sized
+ * vectors; the layer path is bcfft_forward). */
+int bcfft_circulant_matvec(const void* c, const void* x, int dtype, int n, void* y, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BCFFT_H */

@@ -1,0 +1,88 @@
+"""ctypes binding of libbcfft.so (the C ABI declared in include/bcfft.h).
+
+The library is built in-tree (``make -C llama-fft_amd`` or ``__graft_entry__.build()``) into
+``llama-fft_amd/lib/libbcfft.so``. There is no fallback: if the library is missing or a
+call fails, a ``RuntimeError`` is raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libbcfft.so")
+ABI_VERSION = 1
+
+BCFFT_NONE, BCFFT_F32, BCFFT_F16, BCFFT_BF16 = -1, 0, 1, 2
+DTYPE_CODE = {torch.float32: BCFFT_F32, torch.float16: BCFFT_F16, torch.bfloat16: BCFFT_BF16}
+SUPPORTED_BLOCKS = (32, 64, 128, 256)
+
+# every symbol include/bcfft.h declares, with its ctypes signature
+_SIGNATURES = {
+    "bcfft_abi_version": (ctypes.c_int, []),
+    "bcfft_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "bcfft_last_hip_error": (ctypes.c_char_p, []),
+    "bcfft_spectra_bytes": (ctypes.c_int64, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "bcfft_spectra": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    "bcfft_forward": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "bcfft_circulant_matvec": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and return the library; raise RuntimeError if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libbcfft.so not found at {LIB_PATH}: build it with `make -C llama-fft_amd` "
+                "(or __graft_entry__.build()). The MI355X engine has no CPU/torch fallback.")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.bcfft_abi_version() != ABI_VERSION:
+            raise RuntimeError(f"libbcfft ABI {lib.bcfft_abi_version()} != expected {ABI_VERSION}")
+        _lib = lib
+    return _lib
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        lib = load()
+        msg = lib.bcfft_status_string(status).decode()
+        hip = lib.bcfft_last_hip_error().decode()
+        raise RuntimeError(f"{what} failed: {msg}" + (f" ({hip})" if hip else ""))
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    try:
+        return DTYPE_CODE[dt]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {dt}; BC engine supports float32/float16/bfloat16")
+
+
+def stream_handle(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_device(t: torch.Tensor, what: str) -> None:
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            f"{what}: the MI355X BC engine runs on ROCm device tensors only (got {t.device}); "
+            "move the module and inputs to the GPU. There is no CPU path in the product.")

@@ -1,0 +1,76 @@
+"""Tensor-level wrappers over the C ABI (torch is plumbing: allocation, streams, autograd).
+
+Every function here enqueues HIP work on the caller's current stream and returns without
+synchronising. Shapes/dtypes are validated in Python (for the reference's exception types)
+and again in the library (status codes).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+def spectra_numel(n_out_blocks: int, n_in_blocks: int, block_size: int) -> int:
+    nbytes = _lib.load().bcfft_spectra_bytes(n_out_blocks, n_in_blocks, block_size)
+    if nbytes < 0:
+        raise ValueError(f"invalid spectra geometry ({n_out_blocks}, {n_in_blocks}, {block_size})")
+    return nbytes // 4
+
+
+def spectra(c: torch.Tensor, transpose_conj: bool = False) -> torch.Tensor:
+    """Packed weight spectra of c (nO, nI, b) -> flat float32 device buffer.
+
+    Replaces rfft(c.to(fp32)) (patch_llama_fft.py:256-257). transpose_conj=True gives the
+    adjoint operator's spectra (used for dL/dx)."""
+    _lib.require_device(c, "bcfft.spectra")
+    if c.dim() != 3:
+        raise ValueError("c must be (out_blocks, in_blocks, block_size)")
+    n_out, n_in, b = c.shape
+    if b not in _lib.SUPPORTED_BLOCKS:
+        raise ValueError(f"block_size {b} not supported (supported: {_lib.SUPPORTED_BLOCKS})")
+    c = c.detach().contiguous()
+    out = torch.empty(spectra_numel(n_out, n_in, b), dtype=torch.float32, device=c.device)
+    lib = _lib.load()
+    _lib.check(lib.bcfft_spectra(c.data_ptr(), _lib.dtype_code(c.dtype), n_out, n_in, b,
+                                 int(bool(transpose_conj)), out.data_ptr(),
+                                 _lib.stream_handle(c.device)), "bcfft_spectra")
+    return out
+
+
+def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, block_size: int,
+            out_features: int) -> torch.Tensor:
+    """y = BC(x2d) (+ bias) with one fused kernel. x2d: (N, K) device tensor."""
+    _lib.require_device(x2d, "bcfft.forward")
+    n, k = x2d.shape
+    x2d = x2d.contiguous()
+    if x2d.data_ptr() % 16:
+        x2d = x2d.clone()
+    out_dtype = x2d.dtype if bias is None else torch.promote_types(x2d.dtype, bias.dtype)
+    y = torch.empty((n, out_features), dtype=out_dtype, device=x2d.device)
+    if n == 0:
+        return y
+    bias_ptr, bias_code = 0, _lib.BCFFT_NONE
+    if bias is not None:
+        bias = bias.detach().contiguous()
+        bias_ptr, bias_code = bias.data_ptr(), _lib.dtype_code(bias.dtype)
+    lib = _lib.load()
+    _lib.check(lib.bcfft_forward(x2d.data_ptr(), _lib.dtype_code(x2d.dtype), n, k, out_features,
+                                 block_size, spec.data_ptr(), bias_ptr, bias_code, y.data_ptr(),
+                                 _lib.dtype_code(out_dtype), _lib.stream_handle(x2d.device)),
+               "bcfft_forward")
+    return y
+
+
+def circulant_matvec(c: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """y = C(c) x for one circulant of any length (fft_utils.py:3-34)."""
+    _lib.require_device(x, "bcfft.circulant_matvec")
+    dt = x.dtype
+    c = c.to(dt).contiguous()
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    lib = _lib.load()
+    _lib.check(lib.bcfft_circulant_matvec(c.data_ptr(), x.data_ptr(), _lib.dtype_code(dt),
+                                          x.numel(), y.data_ptr(), _lib.stream_handle(x.device)),
+               "bcfft_circulant_matvec")
+    return y

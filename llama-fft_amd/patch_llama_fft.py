@@ -1,0 +1,349 @@
+"""Drop-in replacement for the reference's ``patch_llama_fft`` module on MI355X.
+
+Same public surface as Pinguhat/llama-fft ``src/patch_llama_fft.py`` (cited per symbol;
+paths relative to the reference's ``src/``): ``MODEL_PATH``, ``BLOCK_SIZE``,
+``NUM_LAYERS_TO_PATCH``, ``BlockCirculantLinear`` (ctor, attributes, ``from_linear``,
+``forward``), the circulant projection helpers, ``save_bc_params``/``load_bc_params``,
+``patch_mlp_with_block_circulant`` and ``main``. Put ``llama-fft_amd/`` on ``sys.path`` where
+the reference put ``src/`` and ``import patch_llama_fft`` resolves here.
+
+What differs, by design:
+  * ``BlockCirculantLinear.forward`` runs ONE fused HIP kernel (libbcfft.so,
+    ``bcfft_forward``) on gfx950 instead of torch's rfft/einsum/irfft/cast/add chain. The
+    weight spectra are computed by ``bcfft_spectra`` and cached per module, keyed by the
+    parameter's version counter, so an in-place update of ``c`` can never be served stale
+    (the reference's cached forward can: bench_all_in_one.py:204-216).
+  * There is no CPU path: a non-ROCm tensor raises ``RuntimeError``.
+  * Backward: dL/dx runs the same fused kernel on the adjoint spectra; dL/dc uses torch.fft
+    on the device (scope row f3).
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict
+
+import torch
+import torch.nn as nn
+
+from bcfft import ops as _ops
+from bcfft import _lib
+from fft_utils import circulant_matvec_fft
+
+# Same module constants as the reference (patch_llama_fft.py:10-15)
+MODEL_PATH = os.environ.get("LLAMA_FFT_MODEL_PATH", r"C:\Users\Lukas\Documents\0-UNI\Seminar\Llama2")
+BLOCK_SIZE = 256
+NUM_LAYERS_TO_PATCH = 1
+
+
+# ----------------------------------------------------------------------------- projection helpers
+def _detect_best_convention_for_layer(W: torch.Tensor, block_size: int, *, num_probes: int = 3) -> str:
+    """patch_llama_fft.py:17-44 — pick "diag" or "diag_inv" by probe error on the top-left block."""
+    B = block_size
+    block = W[:B, :B].detach().to(dtype=torch.float32)
+    dev = block.device
+    torch.manual_seed(0)
+    xs = [torch.randn(B, device=dev, dtype=torch.float32) for _ in range(num_probes)]
+
+    def score(convention: str) -> float:
+        c = dense_block_to_circulant_column(block, convention=convention).to(torch.float32)
+        err = 0.0
+        for x in xs:
+            err += (block @ x - circulant_matvec_fft(c, x)).pow(2).mean().item()
+        return err / float(num_probes)
+
+    return "diag" if score("diag") <= score("diag_inv") else "diag_inv"
+
+
+def dense_block_to_circulant_column(W_block: torch.Tensor, *, convention: str = "diag") -> torch.Tensor:
+    """patch_llama_fft.py:47-79 — c[k] = mean_i W[i,(i+k)%B] ("diag") or W[(i+k)%B,i]."""
+    assert W_block.dim() == 2
+    B0, B1 = W_block.shape
+    assert B0 == B1
+    if convention not in ("diag", "diag_inv"):
+        raise ValueError(f"Unknown convention: {convention}")
+    B = B0
+    idx = torch.arange(B, device=W_block.device)
+    k = idx[:, None]
+    if convention == "diag":
+        vals = W_block[idx[None, :], (idx[None, :] + k) % B]
+    else:
+        vals = W_block[(idx[None, :] + k) % B, idx[None, :]]
+    return vals.mean(dim=1).to(W_block.dtype)
+
+
+def _project_loss_aware_batched(blocks: torch.Tensor, eps: float = 1e-12) -> torch.Tensor:
+    """Batched dense_block_to_circulant_column_loss_aware over (..., B, B), in blocks.dtype."""
+    B = blocks.shape[-1]
+    idx = torch.arange(B, device=blocks.device)
+    cols = (idx[None, :] - idx[:, None]) % B                     # [t, r] -> column (r - t) % B
+    diag = blocks[..., idx[None, :], cols]                       # (..., t, r)   :116-117
+    c = diag.mean(dim=-1)                                        # :118
+    diag_sums = diag.sum(dim=-1)                                 # :119
+    numerator = (c * diag_sums).sum(dim=-1)                      # :124
+    denom = (B * (c * c).sum(dim=-1)).clamp_min(eps)             # :125
+    alpha = numerator / denom                                    # :126
+    return (alpha[..., None] * c).to(blocks.dtype)               # :128
+
+
+def dense_block_to_circulant_column_loss_aware(W_block: torch.Tensor, eps: float = 1e-12) -> torch.Tensor:
+    """patch_llama_fft.py:82-128 — Frobenius projection onto circulants (first-column
+    convention C[i,j] = c[(i-j)%B]) with energy-preserving alpha; arithmetic in W's dtype."""
+    assert W_block.dim() == 2
+    B0, B1 = W_block.shape
+    assert B0 == B1
+    return _project_loss_aware_batched(W_block, eps)
+
+
+def circulant_from_first_col(c: torch.Tensor) -> torch.Tensor:
+    """patch_llama_fft.py:132-139 — explicit B x B circulant, C[:, j] = roll(c, j)."""
+    B = c.numel()
+    idx = torch.arange(B, device=c.device)
+    return c[(idx[:, None] - idx[None, :]) % B]
+
+
+# ----------------------------------------------------------------------------- autograd
+class _BCFunction(torch.autograd.Function):
+    """Fused forward on the HIP engine; backward: dx through the fused kernel on adjoint
+    spectra, dc by per-bin cross-correlation (torch.fft on device), dbias by reduction."""
+
+    @staticmethod
+    def forward(ctx, x2d, c, bias, module):
+        spec = module._spectra(c)
+        y = _ops.forward(x2d, spec, bias, module.block_size, module.out_features)
+        ctx.module = module
+        ctx.save_for_backward(x2d, c, bias)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2d, c, bias = ctx.saved_tensors
+        m = ctx.module
+        dx = dc = dbias = None
+        dy = dy.contiguous()
+        if ctx.needs_input_grad[0]:
+            spec_t = m._spectra(c, adjoint=True)
+            dx = _ops.forward(dy, spec_t, None, m.block_size, m.in_features).to(x2d.dtype)
+        if ctx.needs_input_grad[1]:
+            n = x2d.shape[0]
+            b = m.block_size
+            xf = torch.fft.rfft(x2d.to(torch.float32).reshape(n, m.in_blocks, b), dim=-1)
+            dyf = torch.fft.rfft(dy.to(torch.float32).reshape(n, m.out_blocks, b), dim=-1)
+            dcf = torch.einsum("nof,nif->oif", dyf, xf.conj())
+            dc = torch.fft.irfft(dcf, n=b, dim=-1).to(c.dtype)
+        if bias is not None and ctx.needs_input_grad[2]:
+            dbias = dy.sum(dim=0).to(bias.dtype)
+        return dx, dc, dbias, None
+
+
+# ----------------------------------------------------------------------------- the module
+class BlockCirculantLinear(nn.Module):
+    """Block-circulant linear layer (patch_llama_fft.py:142-275), FFT-multiplied on MI355X.
+
+    c[j, i, :] is the first column of the circulant block C_{j,i} mapping input block i to
+    output block j: y_j = sum_i C_{j,i} x_i, C[r, s] = c[(r - s) % block_size].
+    """
+
+    def __init__(self, in_features: int, out_features: int, block_size: int = 256, bias: bool = True):
+        super().__init__()
+        assert in_features % block_size == 0, "in_features must be divisible by block_size"    # :159
+        assert out_features % block_size == 0, "out_features must be divisible by block_size"  # :160
+        self.in_features = in_features
+        self.out_features = out_features
+        self.block_size = block_size
+        self.in_blocks = in_features // block_size
+        self.out_blocks = out_features // block_size
+        self.c = nn.Parameter(torch.randn(self.out_blocks, self.in_blocks, self.block_size) * 0.01)  # :171-173
+        if bias:
+            self.bias = nn.Parameter(torch.zeros(out_features))                               # :175-176
+        else:
+            self.bias = None
+        self._spec_cache: Dict[tuple, torch.Tensor] = {}
+
+    @classmethod
+    def from_linear(cls, linear: nn.Linear, block_size: int = 256) -> "BlockCirculantLinear":
+        """patch_llama_fft.py:180-224 — project every b x b block of the dense weight onto a
+        circulant (loss-aware, in the weight's dtype), keep c in fp32, copy the bias."""
+        in_f, out_f = linear.in_features, linear.out_features
+        layer = cls(in_features=in_f, out_features=out_f, block_size=block_size,
+                    bias=(linear.bias is not None))
+        layer = layer.to(linear.weight.device)                                                # :198
+        with torch.no_grad():
+            W = linear.weight.data
+            B = block_size
+            blocks = W.view(layer.out_blocks, B, layer.in_blocks, B).permute(0, 2, 1, 3)       # :208-209
+            layer.c.data.copy_(_project_loss_aware_batched(blocks))                            # :214-219
+            if layer.bias is not None and linear.bias is not None:
+                layer.bias.data.copy_(linear.bias.data)                                        # :221-222
+        return layer
+
+    # -- spectra cache (device, storage, version, dtype): recomputed after any update of c
+    def _spectra(self, c: torch.Tensor, adjoint: bool = False) -> torch.Tensor:
+        key = (adjoint, c.device, c.data_ptr(), c._version, c.dtype, tuple(c.shape))
+        spec = self._spec_cache.get(key)
+        if spec is None:
+            self._spec_cache = {k: v for k, v in self._spec_cache.items() if k[0] != adjoint}
+            spec = _ops.spectra(c, transpose_conj=adjoint)
+            self._spec_cache[key] = spec
+        return spec
+
+    def _apply(self, fn, *args, **kwargs):  # .to()/.cuda()/.half(): drop device-bound spectra
+        self._spec_cache = {}
+        return super()._apply(fn, *args, **kwargs)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if x.dim() == 3:                                                                       # :228-233
+            bs, sl, in_f = x.shape
+            assert in_f == self.in_features
+            x_flat = x.reshape(bs * sl, in_f)
+            is_3d = True
+        elif x.dim() == 2:                                                                     # :234-238
+            x_flat = x
+            is_3d = False
+        else:
+            raise ValueError("Unsupported input dim")                                          # :239
+        # same error as the reference's reshape (:246) for a 2D input of the wrong width
+        x_flat.reshape(x_flat.shape[0], self.in_blocks, self.block_size)
+        _lib.require_device(x_flat, "BlockCirculantLinear.forward")
+        y_flat = _BCFunction.apply(x_flat, self.c, self.bias, self)
+        if is_3d:
+            return y_flat.view(bs, sl, self.out_features)                                      # :273-274
+        return y_flat
+
+    def extra_repr(self) -> str:
+        return (f"in_features={self.in_features}, out_features={self.out_features}, "
+                f"block_size={self.block_size}, bias={self.bias is not None}, engine=bcfft-gfx950")
+
+
+# ----------------------------------------------------------------------------- param I/O
+def _get_submodule_by_name(model: nn.Module, name: str) -> nn.Module:
+    """patch_llama_fft.py:278-284."""
+    cur = model
+    if name == "":
+        return cur
+    for part in name.split("."):
+        cur = getattr(cur, part)
+    return cur
+
+
+def save_bc_params(model: nn.Module, path: str) -> None:
+    """patch_llama_fft.py:287-300 — {"<module>.c": (nO,nI,b), "<module>.bias": (M,)} via torch.save."""
+    bc_state: Dict[str, torch.Tensor] = {}
+    for module_name, module in model.named_modules():
+        if isinstance(module, BlockCirculantLinear):
+            bc_state[f"{module_name}.c"] = module.c.detach().cpu()
+            if module.bias is not None:
+                bc_state[f"{module_name}.bias"] = module.bias.detach().cpu()
+    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+    torch.save(bc_state, path)
+    print(f"Saved BC params: {len(bc_state)} tensors -> {path}")
+
+
+def load_bc_params(model: nn.Module, path: str, *, strict_shapes: bool = True) -> None:
+    """patch_llama_fft.py:303-340 — load a save_bc_params checkpoint (tensors only:
+    weights_only=True), skipping unknown names and mismatched shapes."""
+    state: Dict[str, torch.Tensor] = torch.load(path, map_location="cpu", weights_only=True)
+    loaded = 0
+    skipped = 0
+    for full_name, tensor in state.items():
+        if not (full_name.endswith(".c") or full_name.endswith(".bias")):
+            skipped += 1
+            continue
+        module_name, param_name = full_name.rsplit(".", 1)
+        try:
+            module = _get_submodule_by_name(model, module_name)
+        except AttributeError:
+            skipped += 1
+            continue
+        if not hasattr(module, param_name):
+            skipped += 1
+            continue
+        param = getattr(module, param_name)
+        if not isinstance(param, torch.Tensor):
+            skipped += 1
+            continue
+        if strict_shapes and param.shape != tensor.shape:
+            skipped += 1
+            continue
+        with torch.no_grad():
+            param.copy_(tensor.to(param.device, dtype=param.dtype))
+        loaded += 1
+    print(f"Loaded BC params from {path}: loaded={loaded}, skipped={skipped}")
+
+
+# ----------------------------------------------------------------------------- model patcher
+MLP_PROJECTIONS = ("gate_proj", "up_proj", "down_proj")
+ATTN_PROJECTIONS = ("q_proj", "k_proj", "v_proj", "o_proj")
+
+
+def _layer_indices(n_layers: int, num_layers_to_patch: int, patch_position: str):
+    if num_layers_to_patch < 0:
+        raise ValueError("num_layers_to_patch must be >= 0")                                   # :361-362
+    k = min(num_layers_to_patch, n_layers)
+    if patch_position not in ("first", "last"):
+        raise ValueError("patch_position must be 'first' or 'last'")                           # :365-366
+    return list(range(k)) if patch_position == "first" else list(range(n_layers - k, n_layers))
+
+
+def _patch(model, layer_indices, block_size, targets):
+    for layer_idx in layer_indices:
+        layer = model.model.layers[layer_idx]
+        for parent_name, names in (("mlp", MLP_PROJECTIONS), ("self_attn", ATTN_PROJECTIONS)):
+            parent = getattr(layer, parent_name, None)
+            if parent is None:
+                continue
+            sel = [n for n in names if n in targets]
+            if sel:
+                print(f"  Patching layer {layer_idx} {parent_name.upper() if parent_name == 'mlp' else parent_name}...")
+            for name in sel:
+                old_layer = getattr(parent, name, None)
+                if not isinstance(old_layer, nn.Linear):
+                    print(f"    Skip {name}: not an nn.Linear")
+                    continue
+                print(f"    Replacing {name}: in_features={old_layer.in_features}, "
+                      f"out_features={old_layer.out_features}")
+                setattr(parent, name, BlockCirculantLinear.from_linear(old_layer, block_size=block_size))
+
+
+def patch_mlp_with_block_circulant(model, *, num_layers_to_patch: int = NUM_LAYERS_TO_PATCH,
+                                   block_size: int = BLOCK_SIZE, patch_position: str = "first") -> None:
+    """patch_llama_fft.py:343-394 — replace gate/up/down_proj of the first/last k decoder
+    layers with BlockCirculantLinear.from_linear(...)."""
+    n_layers = model.config.num_hidden_layers
+    print(f"Model has {n_layers} transformer layers.")
+    layer_indices = _layer_indices(n_layers, num_layers_to_patch, patch_position)
+    print(f"Patching {len(layer_indices)} layer(s) from {patch_position}: {layer_indices}")
+    _patch(model, layer_indices, block_size, MLP_PROJECTIONS)
+
+
+def patch_linear_with_block_circulant(model, *, num_layers_to_patch: int = NUM_LAYERS_TO_PATCH,
+                                      block_size: int = BLOCK_SIZE, patch_position: str = "first",
+                                      targets=MLP_PROJECTIONS + ATTN_PROJECTIONS) -> None:
+    """Extension for BASELINE config 3 ("all linear layers BC"): also q/k/v/o_proj. Same
+    kwargs as patch_mlp_with_block_circulant so signature-introspecting harnesses
+    (bench_all_in_one.py:127-139) can call either."""
+    n_layers = model.config.num_hidden_layers
+    print(f"Model has {n_layers} transformer layers.")
+    layer_indices = _layer_indices(n_layers, num_layers_to_patch, patch_position)
+    print(f"Patching {len(layer_indices)} layer(s) from {patch_position}: {layer_indices}")
+    _patch(model, layer_indices, block_size, tuple(targets))
+
+
+def main():
+    """patch_llama_fft.py:396-419 — load LLaMA from MODEL_PATH, patch, run a shape check."""
+    from transformers import AutoModelForCausalLM
+    print(f"Loading Llama-2-7b from local path: {MODEL_PATH}")
+    model = AutoModelForCausalLM.from_pretrained(MODEL_PATH, device_map="cpu", torch_dtype=torch.float16,
+                                                 low_cpu_mem_usage=True, local_files_only=True)
+    model.eval()
+    patch_mlp_with_block_circulant(model)
+    model = model.to("cuda")
+    print("Running a small forward pass to check shapes...")
+    input_ids = torch.randint(0, model.config.vocab_size, (1, 8), device="cuda")
+    with torch.no_grad():
+        outputs = model(input_ids=input_ids)
+    print("Forward pass completed.")
+    print("Logits shape:", outputs.logits.shape)
+
+
+if __name__ == "__main__":
+    main()

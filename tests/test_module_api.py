@@ -1,0 +1,122 @@
+"""The drop-in module surface (patch_llama_fft / fft_utils) on the CPU: constructor contract,
+weight preparation (from_linear) against the reference's golden vectors, param I/O format and
+the model patcher on a tiny locally-built LLaMA. No kernel runs here."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from golden_io import load, names, rel_err
+
+
+@pytest.fixture(scope="module")
+def plf(built_lib):
+    import patch_llama_fft
+    return patch_llama_fft
+
+
+def test_constructor_contract(plf):
+    m = plf.BlockCirculantLinear(512, 256, block_size=128)
+    assert (m.in_features, m.out_features, m.block_size) == (512, 256, 128)
+    assert (m.in_blocks, m.out_blocks) == (4, 2)
+    assert m.c.shape == (2, 4, 128) and m.c.dtype == torch.float32
+    assert m.bias.shape == (256,) and torch.all(m.bias == 0)
+    assert 0.005 < m.c.std().item() < 0.02                       # randn * 0.01 (:171-173)
+    assert set(m.state_dict()) == {"c", "bias"}
+    assert plf.BlockCirculantLinear(256, 256, block_size=64, bias=False).bias is None
+    with pytest.raises(AssertionError, match="in_features must be divisible"):
+        plf.BlockCirculantLinear(100, 256, block_size=64)
+    with pytest.raises(AssertionError, match="out_features must be divisible"):
+        plf.BlockCirculantLinear(256, 100, block_size=64)
+    assert plf.BLOCK_SIZE == 256 and plf.NUM_LAYERS_TO_PATCH == 1
+
+
+def test_default_block_size(plf):
+    assert plf.BlockCirculantLinear(512, 512).block_size == 256
+
+
+@pytest.mark.parametrize("name", names("from_linear_"))
+def test_from_linear_vs_reference_golden(plf, name):
+    g = load(name)
+    dt = {"float32": torch.float32, "float16": torch.float16}[g["w__dt"]]
+    m, k = g["w"].shape
+    lin = torch.nn.Linear(k, m, bias="lin_bias" in g).to(dt)
+    with torch.no_grad():
+        lin.weight.copy_(torch.from_numpy(g["w"]))
+        if "lin_bias" in g:
+            lin.bias.copy_(torch.from_numpy(g["lin_bias"]))
+    bc = plf.BlockCirculantLinear.from_linear(lin, block_size=int(g["block_size"]))
+    assert bc.c.dtype == torch.float32                            # c stays fp32 (:192-198)
+    tol = 1e-6 if dt == torch.float32 else 1e-3
+    assert rel_err(bc.c.detach().numpy(), g["c"]) < tol
+    if "bias" in g:
+        assert np.array_equal(bc.bias.detach().numpy(), g["bias"])
+
+
+def test_projection_helpers(plf):
+    g = load("project_t2_exact")
+    c = plf.dense_block_to_circulant_column_loss_aware(torch.from_numpy(g["w"]))
+    assert torch.allclose(c, torch.from_numpy(g["c"]), rtol=1e-6, atol=1e-6)
+    c0 = torch.randn(16)
+    C = plf.circulant_from_first_col(c0)
+    idx = torch.arange(16)
+    assert torch.equal(C, c0[(idx[:, None] - idx[None, :]) % 16])
+    assert torch.allclose(plf.dense_block_to_circulant_column(C.T.contiguous()), c0, atol=1e-6)
+    with pytest.raises(ValueError):
+        plf.dense_block_to_circulant_column(C, convention="bogus")
+
+
+def test_save_load_roundtrip(plf, tmp_path):
+    net = torch.nn.Sequential(plf.BlockCirculantLinear(256, 128, block_size=64),
+                              plf.BlockCirculantLinear(128, 256, block_size=64, bias=False))
+    p = os.path.join(tmp_path, "sub", "bc.pt")
+    plf.save_bc_params(net, p)
+    state = torch.load(p, weights_only=True)
+    assert set(state) == {"0.c", "0.bias", "1.c"}
+    net2 = torch.nn.Sequential(plf.BlockCirculantLinear(256, 128, block_size=64),
+                               plf.BlockCirculantLinear(128, 256, block_size=64, bias=False))
+    plf.load_bc_params(net2, p)
+    assert torch.equal(net2[0].c, net[0].c) and torch.equal(net2[1].c, net[1].c)
+    # mismatched shape is skipped under strict_shapes
+    net3 = torch.nn.Sequential(plf.BlockCirculantLinear(256, 128, block_size=32))
+    plf.load_bc_params(net3, p)
+    assert not torch.equal(net3[0].c.flatten()[:10], net[0].c.flatten()[:10])
+
+
+def _tiny_llama():
+    from transformers import LlamaConfig, LlamaForCausalLM
+    cfg = LlamaConfig(vocab_size=64, hidden_size=256, intermediate_size=512, num_hidden_layers=3,
+                      num_attention_heads=4, num_key_value_heads=4, max_position_embeddings=64)
+    torch.manual_seed(0)
+    return LlamaForCausalLM(cfg).eval()
+
+
+def test_patch_mlp_first_last(plf):
+    model = _tiny_llama()
+    plf.patch_mlp_with_block_circulant(model, num_layers_to_patch=2, block_size=128, patch_position="last")
+    kinds = [type(l.mlp.up_proj).__name__ for l in model.model.layers]
+    assert kinds == ["Linear", "BlockCirculantLinear", "BlockCirculantLinear"]
+    assert type(model.model.layers[2].self_attn.q_proj).__name__ == "Linear"
+    with pytest.raises(ValueError):
+        plf.patch_mlp_with_block_circulant(model, num_layers_to_patch=-1)
+    with pytest.raises(ValueError):
+        plf.patch_mlp_with_block_circulant(model, patch_position="middle")
+
+
+def test_patch_all_linear(plf):
+    model = _tiny_llama()
+    plf.patch_linear_with_block_circulant(model, num_layers_to_patch=1, block_size=64)
+    l0 = model.model.layers[0]
+    for name in ("q_proj", "k_proj", "v_proj", "o_proj"):
+        assert isinstance(getattr(l0.self_attn, name), plf.BlockCirculantLinear)
+    assert isinstance(l0.mlp.down_proj, plf.BlockCirculantLinear)
+    assert l0.mlp.down_proj.bias is None                           # LLaMA: mlp_bias=False
+
+
+def test_forward_refuses_cpu(plf):
+    m = plf.BlockCirculantLinear(128, 128, block_size=64)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        m(torch.zeros(2, 128))
+    with pytest.raises(ValueError, match="Unsupported input dim"):
+        m(torch.zeros(128))
