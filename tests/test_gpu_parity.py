@@ -29,7 +29,7 @@ def _to_dev(a, dtname, dev):
 
 
 def _check(got: torch.Tensor, ref: np.ndarray, out_dt: str, tol=TOL_F32):
-    g = got.float().cpu().numpy()
+    g = got.detach().float().cpu().numpy()
     assert g.shape == ref.shape
     assert np.isfinite(g).all()
     e = rel_err(g, ref)
