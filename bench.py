@@ -154,6 +154,7 @@ def main():
         barrier = None
 
     n, k, m, b, io = args.tokens, args.in_features, args.out_features, args.block_size, args.io
+    algo = os.environ.setdefault("BCFFT_ALGO", "auto")
     layer = make_layer(k, m, b, io, bool(args.bias), dev)
     torch.manual_seed(1000 + rank)                           # x ~ N(0,1) per rank shard
     x = torch.randn(n, k, device=dev).to(DT[io])
@@ -192,13 +193,19 @@ def main():
 
     variants = []
     if args.variants and rank == 0 and world == 1:
-        for (vk, vm, vb, vio, vn) in [(4096, 4096, 128, "bf16", 8192), (4096, 11008, 128, "bf16", 8192),
-                                      (4096, 4096, 64, "fp32", 8192), (4096, 4096, 256, "fp32", 8192)]:
+        for (vk, vm, vb, vio, vn, va) in [(4096, 4096, 128, "fp32", 8192, "valu"),
+                                          (4096, 4096, 128, "bf16", 8192, "auto"),
+                                          (4096, 11008, 128, "bf16", 8192, "auto"),
+                                          (11008, 4096, 128, "bf16", 8192, "auto"),
+                                          (4096, 4096, 64, "fp32", 8192, "auto"),
+                                          (4096, 4096, 256, "fp32", 8192, "auto")]:
+            os.environ["BCFFT_ALGO"] = va
             vl = make_layer(vk, vm, vb, vio, False, dev)
             vx = torch.randn(vn, vk, device=dev).to(DT[vio])
             vw, vkern = time_layer(vl, vx, max(10, args.steps // 2), 5)
+            os.environ["BCFFT_ALGO"] = algo
             vbytes = algo_bytes(vn, vk, vm, vb, vio, False)
-            variants.append({"workload": f"{vk}->{vm} b={vb} N={vn} {vio}-io",
+            variants.append({"workload": f"{vk}->{vm} b={vb} N={vn} {vio}-io algo={va}",
                              "ms": round(vkern, 4),
                              "GTok_elem_s": round(vn * vm / (vkern * 1e-3) / 1e9, 3),
                              "GB_s": round(vbytes / (vkern * 1e-3) / 1e9, 1),
@@ -228,7 +235,9 @@ def main():
                                    f"{io} I/O, spectra cached",
                        "in_features": k, "out_features": m, "block_size": b,
                        "tokens_per_rank": n, "global_tokens": n * world, "io_dtype": io,
-                       "bias": bool(args.bias), "parallelism": f"token-shard x{world}"},
+                       "bias": bool(args.bias), "parallelism": f"token-shard x{world}",
+                       "algo": algo, "mac": "MFMA bf16 hi/lo split (Xhi+Xlo)(Chi+Clo), f32 accumulate"
+                       if (algo in ("auto", "mfma") and b <= 128) else "VALU fp32 FMA"},
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                          "traffic": load_traffic(tag),

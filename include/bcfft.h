@@ -30,6 +30,13 @@ extern "C" {
 
 enum bcfft_dtype { BCFFT_NONE = -1, BCFFT_F32 = 0, BCFFT_F16 = 1, BCFFT_BF16 = 2 };
 
+/* Forward algorithms (bcfft_forward_algo). Both are single fused launches.
+ *  MFMA: per-bin complex MAC on the matrix cores as a bf16 GEMM with hi/lo splitting of both
+ *        operands ((Xhi+Xlo)(Chi+Clo), fp32 accumulate; ~1e-5 relative). block_size <= 128.
+ *  VALU: per-bin complex MAC in fp32 FMAs (the reference's fp32 arithmetic). Any block size.
+ *  AUTO: MFMA for block_size <= 128, VALU otherwise. */
+enum bcfft_algo { BCFFT_ALGO_AUTO = 0, BCFFT_ALGO_MFMA = 1, BCFFT_ALGO_VALU = 2 };
+
 enum bcfft_status {
   BCFFT_OK = 0,
   BCFFT_ERR_SHAPE = 1,   /* features not divisible by block_size, non-positive sizes      */
@@ -49,19 +56,22 @@ const char* bcfft_status_string(int status);
 /* Text of the last HIP error seen by this thread (empty if none). */
 const char* bcfft_last_hip_error(void);
 
-/* Bytes of the packed spectra buffer for an (n_out_blocks x n_in_blocks) grid of b x b
- * circulant blocks: n_out*n_in*(b/2) complex64 packed bins + a b-entry twiddle table. */
+/* Bytes of the spectra buffer of an operator with (n_out_blocks x n_in_blocks) b x b
+ * circulant blocks: packed fp32 bins (n_out*n_in*b/2 complex64), a b-entry twiddle table
+ * and, for b <= 128, the split-bf16 image the MFMA kernel streams. */
 int64_t bcfft_spectra_bytes(int n_out_blocks, int n_in_blocks, int block_size);
 
 /* Packed weight spectra. Replaces `Cf = torch.fft.rfft(self.c.to(float32), dim=-1)`
  * (patch_llama_fft.py:256-257) and the memoised Cf of the cached forward
  * (bench_all_in_one.py:204-216).
- *   c:        (n_out_blocks, n_in_blocks, block_size) contiguous, dtype c_dtype
- *   spectra:  bcfft_spectra_bytes(...) bytes, 16-B aligned; receives
- *             S[o][i][k] = rfft(c[o,i])[k] / (2b) for 0<k<b/2, S[o][i][0] = (X0, X_{b/2})/(2b)
- *   transpose_conj = 1 writes the adjoint layout S[i][o][k] = conj(...) instead (the
- *             spectra of the transposed operator, used for dL/dx in the backward pass).
- * Computed in fp64 and rounded once to fp32. */
+ * n_out_blocks / n_in_blocks describe the OPERATOR whose spectra are built:
+ *   transpose_conj = 0: the layer itself; c is (n_out_blocks, n_in_blocks, block_size).
+ *   transpose_conj = 1: its adjoint (used for dL/dx in the backward pass); c is the layer's
+ *                       (n_in_blocks, n_out_blocks, block_size) tensor and the operator's
+ *                       block (o, i) is conj(spectrum of c[i, o]).
+ *   spectra:  bcfft_spectra_bytes(n_out_blocks, n_in_blocks, block_size) bytes, 16-B aligned;
+ *             S[o][i][k] = rfft(c_op[o,i])[k] / (2b) for 0<k<b/2, S[o][i][0] = (X0, X_{b/2})/(2b)
+ * Computed in fp64 and rounded once to fp32 (the bf16 image is split from those values). */
 int bcfft_spectra(const void* c, int c_dtype, int n_out_blocks, int n_in_blocks, int block_size,
                   int transpose_conj, void* spectra, void* stream);
 
@@ -76,6 +86,11 @@ int bcfft_spectra(const void* c, int c_dtype, int n_out_blocks, int n_in_blocks,
 int bcfft_forward(const void* x, int x_dtype, int64_t n_tokens, int in_features,
                   int out_features, int block_size, const void* spectra, const void* bias,
                   int bias_dtype, void* y, int y_dtype, void* stream);
+
+/* bcfft_forward with an explicit algorithm (enum bcfft_algo). */
+int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_features,
+                       int out_features, int block_size, const void* spectra, const void* bias,
+                       int bias_dtype, void* y, int y_dtype, int algo, void* stream);
 
 /* Single circulant matvec y = C(c) x, C[i,j] = c[(i-j) mod n], any n >= 1.
  * Replaces fft_utils.circulant_matvec_fft (fft_utils.py:3-34); c, x, y share `dtype`.

@@ -13,10 +13,12 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libbcfft.so")
+LIB_PATH = os.environ.get("BCFFT_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "lib", "libbcfft.so")
 ABI_VERSION = 1
 
 BCFFT_NONE, BCFFT_F32, BCFFT_F16, BCFFT_BF16 = -1, 0, 1, 2
+ALGO_AUTO, ALGO_MFMA, ALGO_VALU = 0, 1, 2
+ALGOS = {"auto": ALGO_AUTO, "mfma": ALGO_MFMA, "valu": ALGO_VALU}
 DTYPE_CODE = {torch.float32: BCFFT_F32, torch.float16: BCFFT_F16, torch.bfloat16: BCFFT_BF16}
 SUPPORTED_BLOCKS = (32, 64, 128, 256)
 
@@ -31,6 +33,10 @@ _SIGNATURES = {
     "bcfft_forward": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "bcfft_forward_algo": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_void_p]),
     "bcfft_circulant_matvec": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                               ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
 }

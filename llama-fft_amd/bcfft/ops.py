@@ -27,6 +27,8 @@ def spectra(c: torch.Tensor, transpose_conj: bool = False) -> torch.Tensor:
     if c.dim() != 3:
         raise ValueError("c must be (out_blocks, in_blocks, block_size)")
     n_out, n_in, b = c.shape
+    if transpose_conj:                       # the adjoint operator has the swapped grid
+        n_out, n_in = n_in, n_out
     if b not in _lib.SUPPORTED_BLOCKS:
         raise ValueError(f"block_size {b} not supported (supported: {_lib.SUPPORTED_BLOCKS})")
     c = c.detach().contiguous()
@@ -38,9 +40,19 @@ def spectra(c: torch.Tensor, transpose_conj: bool = False) -> torch.Tensor:
     return out
 
 
+def default_algo() -> str:
+    """BCFFT_ALGO env var: auto (default) | mfma | valu."""
+    import os
+    a = os.environ.get("BCFFT_ALGO", "auto").lower()
+    if a not in _lib.ALGOS:
+        raise ValueError(f"BCFFT_ALGO={a!r}: expected one of {sorted(_lib.ALGOS)}")
+    return a
+
+
 def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, block_size: int,
-            out_features: int) -> torch.Tensor:
-    """y = BC(x2d) (+ bias) with one fused kernel. x2d: (N, K) device tensor."""
+            out_features: int, algo: str | None = None) -> torch.Tensor:
+    """y = BC(x2d) (+ bias) with one fused kernel. x2d: (N, K) device tensor.
+    algo: "auto" (MFMA for b <= 128), "mfma" or "valu" (exact fp32 MAC)."""
     _lib.require_device(x2d, "bcfft.forward")
     n, k = x2d.shape
     x2d = x2d.contiguous()
@@ -55,9 +67,10 @@ def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, bl
         bias = bias.detach().contiguous()
         bias_ptr, bias_code = bias.data_ptr(), _lib.dtype_code(bias.dtype)
     lib = _lib.load()
-    _lib.check(lib.bcfft_forward(x2d.data_ptr(), _lib.dtype_code(x2d.dtype), n, k, out_features,
-                                 block_size, spec.data_ptr(), bias_ptr, bias_code, y.data_ptr(),
-                                 _lib.dtype_code(out_dtype), _lib.stream_handle(x2d.device)),
+    code = _lib.ALGOS[(algo or default_algo()).lower()]
+    _lib.check(lib.bcfft_forward_algo(x2d.data_ptr(), _lib.dtype_code(x2d.dtype), n, k, out_features,
+                                      block_size, spec.data_ptr(), bias_ptr, bias_code, y.data_ptr(),
+                                      _lib.dtype_code(out_dtype), code, _lib.stream_handle(x2d.device)),
                "bcfft_forward")
     return y
 

@@ -2,27 +2,35 @@
 //
 // Hot path: BlockCirculantLinear.forward of the reference (patch_llama_fft.py:226-275):
 //   y[n, o*b:(o+1)*b] = sum_i C(c[o,i]) x[n, i*b:(i+1)*b] (+ bias),  C[r,s] = c[(r-s) mod b]
-// computed as rfft -> per-bin complex MAC over input blocks -> irfft, all in ONE launch:
+// computed as rfft -> per-bin complex MAC over input blocks -> irfft, in ONE launch.
 //
-//   per workgroup: TT=16 tokens x OUT_PER_WG output blocks, 512 threads (8 waves)
-//   loop over chunks of IC input blocks:
+// Two forward kernels share the FFT building blocks below:
+//   * bc_forward_mfma_kernel (BCFFT_ALGO_MFMA, default for b <= 128): the per-bin complex MAC
+//     runs on the matrix cores as a dense bf16 GEMM with 4-term hi/lo splitting
+//     ((Xhi+Xlo)(Chi+Clo), fp32 accumulate, ~1e-5 relative), the FFTs on the VALU.
+//   * bc_forward_valu_kernel (BCFFT_ALGO_VALU): the complex MAC in fp32 FMAs (exact fp32
+//     arithmetic, the reference's precision); also the b = 256 path.
+//
+// Per workgroup: TT = 16 tokens x OUT_PER_WG output blocks, 512 threads (8 waves):
+//   loop over chunks of input blocks:
 //     x chunk  --(16 B/lane coalesced loads, prefetched one chunk ahead)--> LDS rows
 //     real FFT of every (token, block) row: b/2-point complex FFT of z = x_even + i x_odd,
-//        four-step L x P with an L-lane group per transform, untangled into packed bins
-//        (bin 0 carries (X_0, X_{b/2}), both real) -> Xf chunk in LDS [block][bin][token]
-//     CMAC on the VALU: lane = bin, registers hold acc[bin][out][token] (128 fp32/lane);
-//        weight spectra (fp32, L2-resident) streamed straight to registers.
-//   epilogue: per output round, accumulators -> LDS rows -> inverse four-step FFT ->
-//        cast to x dtype, + bias, cast to y dtype -> 16 B stores.
-//
+//        four-step L x P, an L-lane group per transform, untangled into packed bins
+//        (bin 0 carries (X_0, X_{b/2}), both real)
+//     complex MAC into register accumulators (MFMA or VALU)
+//   epilogue: accumulators -> LDS rows -> inverse four-step FFT -> cast to x dtype, + bias,
+//        cast to y dtype -> 16 B stores.
 // The 1/b of irfft and the 1/2 of the real-FFT untangling are folded into the spectra.
-// See DESIGN.md for the data layout and the roofline accounting.
+// DESIGN.md has the layouts and the roofline accounting.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "bcfft.h"
 
 namespace bcfft {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 // ------------------------------------------------------------------ scalar conversions
 __device__ __forceinline__ float bf16_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
@@ -54,6 +62,13 @@ __device__ __forceinline__ float load_scalar(const void* p, int64_t i, int dt) {
   if (dt == BCFFT_F32) return ((const float*)p)[i];
   uint32_t h = ((const uint16_t*)p)[i];
   return dt == BCFFT_BF16 ? bf16_to_f32(h) : f16_to_f32(h);
+}
+// v = hi + lo with hi, lo bf16: returns packed (lo16 = first, hi16 = second) pairs
+__device__ __forceinline__ void split_bf16(float2 v, uint32_t& hi, uint32_t& lo) {
+  const uint32_t hx = f32_to_bf16(v.x), hy = f32_to_bf16(v.y);
+  const uint32_t lx = f32_to_bf16(v.x - bf16_to_f32(hx)), ly = f32_to_bf16(v.y - bf16_to_f32(hy));
+  hi = hx | (hy << 16);
+  lo = lx | (ly << 16);
 }
 
 // ------------------------------------------------------------------ complex helpers
@@ -128,13 +143,194 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// ------------------------------------------------------------------ geometry
+// ------------------------------------------------------------------ FFT building blocks
+// One transform per L-lane group, on an LDS row of SROW floats.
 template <int B>
-struct Geo {
+struct Fft {
   static constexpr int H = B / 2;                 // complex FFT length / packed bins
   static constexpr int L = (H <= 32) ? 4 : 8;     // lanes per transform (four-step H = L x P)
   static constexpr int P = H / L;                 // points per lane
   static constexpr int Q = P / L > 0 ? P / L : 1; // k2 values per lane in step 2
+  static constexpr int ROWA = B + 2 * L;
+  static constexpr int ROWB = 2 * P * (L + 1);
+  static constexpr int SROW = ((ROWA > ROWB ? ROWA : ROWB) + 3) / 4 * 4;
+
+  // steps 1-2 of the four-step FFT on v (v[n2] = z[gl + L*n2]); on return the row holds
+  // the result in natural order (complex index k at floats 2k, 2k+1).
+  template <bool INV>
+  static __device__ __forceinline__ void core(float* row, int gl, const float2* tw, float2 (&v)[P]) {
+    dft<P, INV>(v);
+#pragma unroll
+    for (int k2 = 1; k2 < P; ++k2) {                                  // W_H^(+-n1 k2)
+      const float2 w = tw[(2 * gl * k2) % B];
+      v[k2] = INV ? cmulc(v[k2], w) : cmul(v[k2], w);
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int k2 = 0; k2 < P; ++k2)                                    // transpose through the row
+      *reinterpret_cast<float2*>(row + 2 * (k2 * (L + 1) + gl)) = v[k2];
+    wave_lds_sync();
+    float2 u[Q][L];
+#pragma unroll
+    for (int m = 0; m < Q; ++m)
+#pragma unroll
+      for (int n1 = 0; n1 < L; ++n1)
+        u[m][n1] = *reinterpret_cast<const float2*>(row + 2 * ((gl + L * m) * (L + 1) + n1));
+#pragma unroll
+    for (int m = 0; m < Q; ++m) dft<L, INV>(u[m]);
+    wave_lds_sync();
+#pragma unroll
+    for (int m = 0; m < Q; ++m)
+#pragma unroll
+      for (int k1 = 0; k1 < L; ++k1)                                  // index P*k1 + k2
+        *reinterpret_cast<float2*>(row + 2 * (P * k1 + gl + L * m)) = u[m][k1];
+    wave_lds_sync();
+  }
+
+  // forward: row holds x (B reals, fp32 or the raw 16-bit input when RAW16 is the dtype);
+  // afterwards Z = FFT_H(x_even + i x_odd) in natural order (fp32 complex)
+  template <int RAW = BCFFT_F32>
+  static __device__ __forceinline__ void forward(float* row, int gl, const float2* tw) {
+    float2 v[P];
+#pragma unroll
+    for (int n2 = 0; n2 < P; ++n2) {
+      const int j = gl + L * n2;
+      if constexpr (RAW == BCFFT_F32) {
+        v[n2] = *reinterpret_cast<const float2*>(row + 2 * j);
+      } else {
+        const uint32_t w = reinterpret_cast<const uint32_t*>(row)[j];
+        v[n2] = RAW == BCFFT_BF16 ? make_float2(bf16_to_f32(w & 0xffffu), bf16_to_f32(w >> 16))
+                                  : make_float2(f16_to_f32(w & 0xffffu), f16_to_f32(w >> 16));
+      }
+    }
+    core<false>(row, gl, tw, v);
+  }
+
+  // packed spectrum X'[k] = 2 X[k] (bin 0: (2 X_0, 2 X_{H})) from Z in the row
+  static __device__ __forceinline__ float2 untangle(const float* row, int k, const float2* tw) {
+    const float2 zk = *reinterpret_cast<const float2*>(row + 2 * k);
+    const float2 zh = *reinterpret_cast<const float2*>(row + 2 * ((H - k) & (H - 1)));
+    const float sr = zk.x + zh.x, si = zk.y - zh.y;   // Zk + conj(Z[H-k])
+    const float dr = zk.x - zh.x, di = zk.y + zh.y;   // Zk - conj(Z[H-k])
+    const float2 w = tw[k];
+    float2 o;
+    o.x = sr + w.x * di + w.y * dr;                    // (Zk+Zm) - i W^k (Zk-Zm)
+    o.y = si - w.x * dr + w.y * di;
+    if (k == 0) o = make_float2(2.f * (zk.x + zk.y), 2.f * (zk.x - zk.y));
+    return o;
+  }
+
+  // inverse: the row holds packed Y (complex index k stored at column k ^ swz); afterwards
+  // it holds the b real outputs y[0..B) in order (1/b already folded into the spectra).
+  static __device__ __forceinline__ void inverse(float* row, int gl, const float2* tw, int swz) {
+    float2 v[P];
+#pragma unroll
+    for (int n2 = 0; n2 < P; ++n2) {
+      const int k = gl + L * n2;
+      const float2 yk = *reinterpret_cast<const float2*>(row + 2 * (k ^ swz));
+      const float2 yh = *reinterpret_cast<const float2*>(row + 2 * (((H - k) & (H - 1)) ^ swz));
+      const float er = yk.x + yh.x, ei = yk.y - yh.y;   // E = Y[k] + conj(Y[H-k])
+      const float dr = yk.x - yh.x, di = yk.y + yh.y;   // D = Y[k] - conj(Y[H-k])
+      const float2 w = tw[k];                           // O = D conj(W^k); Zi = E + iO
+      float2 z;
+      z.x = er - (di * w.x - dr * w.y);
+      z.y = ei + (dr * w.x + di * w.y);
+      if (k == 0) z = make_float2(yk.x + yk.y, yk.x - yk.y);   // packed bin 0
+      v[n2] = z;
+    }
+    core<true>(row, gl, tw, v);
+  }
+
+  // epilogue store of one transform's b outputs: y32 -> x dtype -> + bias -> y dtype
+  template <int XT>
+  static __device__ __forceinline__ void store(const float* row, int gl, void* yv, int64_t off,
+                                               const void* bias, int64_t bcol, int bias_dt, int y_dt) {
+#pragma unroll
+    for (int pc = 0; pc < B / (4 * L); ++pc) {
+      const int p4 = (gl + L * pc) * 4;
+      const float4 val = *reinterpret_cast<const float4*>(row + p4);
+      float vv[4] = {val.x, val.y, val.z, val.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float r = round_to(vv[e], XT);                                         // .to(x.dtype) :266
+        if (bias_dt != BCFFT_NONE) r += load_scalar(bias, bcol + p4 + e, bias_dt);  // + bias :270-271
+        vv[e] = r;
+      }
+      if (y_dt == BCFFT_F32) {
+        *reinterpret_cast<float4*>((float*)yv + off + p4) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+      } else {
+        uint32_t h[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) h[e] = y_dt == BCFFT_BF16 ? f32_to_bf16(vv[e]) : f32_to_f16(vv[e]);
+        *reinterpret_cast<uint2*>((uint16_t*)yv + off + p4) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+      }
+    }
+  }
+};
+
+template <int XT> struct XTraits;
+template <> struct XTraits<BCFFT_F32> { static constexpr int ES = 4; };
+template <> struct XTraits<BCFFT_F16> { static constexpr int ES = 2; };
+template <> struct XTraits<BCFFT_BF16> { static constexpr int ES = 2; };
+
+// 16 B of x (VEC elements) -> fp32 in LDS
+template <int XT>
+__device__ __forceinline__ void stage_store(float* dst, uint4 v) {
+  if constexpr (XT == BCFFT_F32) {
+    *reinterpret_cast<uint4*>(dst) = v;
+  } else {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    float f[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if constexpr (XT == BCFFT_BF16) {
+        f[2 * k] = bf16_to_f32(w[k] & 0xffffu);
+        f[2 * k + 1] = bf16_to_f32(w[k] >> 16);
+      } else {
+        f[2 * k] = f16_to_f32(w[k] & 0xffffu);
+        f[2 * k + 1] = f16_to_f32(w[k] >> 16);
+      }
+    }
+    *reinterpret_cast<float4*>(dst) = make_float4(f[0], f[1], f[2], f[3]);
+    *reinterpret_cast<float4*>(dst + 4) = make_float4(f[4], f[5], f[6], f[7]);
+  }
+}
+
+// ------------------------------------------------------------------ spectra buffer layout
+// [packed fp32: nO*nI*H float2][twiddles: B float2][MFMA image (b <= 128)]
+// MFMA image: dword ((c*H + f)*2 + prec)*nOp*8 + o*8 + j  = split-bf16 pair of bin f of
+// block (o, 8c + j): bin 0 (C0, C_H) as is, other bins conj(C); prec 0 = hi, 1 = lo.
+struct SpecLayout {
+  int64_t packed_f2, tw_off_f2, img_off_u32, img_u32, total_bytes;
+  int n_chunk, n_out_pad;
+};
+__host__ __device__ inline int mfma_out_per_wg(int b) { return 4096 / b; }   // 16 * NTL
+__host__ __device__ inline SpecLayout spec_layout(int n_out, int n_in, int b) {
+  SpecLayout s;
+  const int h = b / 2;
+  s.packed_f2 = (int64_t)n_out * n_in * h;
+  s.tw_off_f2 = s.packed_f2;
+  const int64_t head_f2 = s.packed_f2 + b;
+  s.img_off_u32 = head_f2 * 2;
+  if (b <= 128) {
+    const int opw = mfma_out_per_wg(b);
+    s.n_chunk = (n_in + 7) / 8;
+    s.n_out_pad = (n_out + opw - 1) / opw * opw;
+    s.img_u32 = (int64_t)s.n_chunk * h * 2 * s.n_out_pad * 8;
+  } else {
+    s.n_chunk = 0;
+    s.n_out_pad = 0;
+    s.img_u32 = 0;
+  }
+  s.total_bytes = head_f2 * 8 + s.img_u32 * 4;
+  return s;
+}
+
+// ================================================================== VALU forward kernel
+template <int B>
+struct GeoV {
+  using F = Fft<B>;
+  static constexpr int H = B / 2, L = F::L, SROW = F::SROW;
   static constexpr int LBINS = H < 64 ? H : 64;   // bins covered by one pass of 64 lanes
   static constexpr int BPL = H / LBINS;           // bins per lane
   static constexpr int LS = 64 / LBINS;           // lane sub-groups (outputs) per wave
@@ -145,74 +341,54 @@ struct Geo {
   static constexpr int OUT_PER_WG = NW * LS * OPL;
   static constexpr int NGROUPS = NT / L;          // FFT groups in the workgroup
   static constexpr int IC = NGROUPS / TT;         // input blocks per chunk
-  // LDS row (floats) of one transform: staging / transpose / natural-order scratch
-  static constexpr int ROWA = B + 2 * L;
-  static constexpr int ROWB = 2 * P * (L + 1);
-  static constexpr int SROW = ((ROWA > ROWB ? ROWA : ROWB) + 3) / 4 * 4;
   static constexpr int XROW = 2 * (TT + 2);       // floats per (block, bin) row of Xf
-  // LDS carve (floats)
-  static constexpr int TW_OFF = 0;                          // B float2 twiddles
-  static constexpr int MAIN_OFF = 2 * B;
-  static constexpr int STAGE_FLOATS = NGROUPS * SROW;       // x staging / FFT scratch
+  static constexpr int MAIN_OFF = 2 * B;          // after B float2 twiddles
+  static constexpr int STAGE_FLOATS = NGROUPS * SROW;
   static constexpr int XF_OFF = MAIN_OFF + STAGE_FLOATS;
   static constexpr int XF_FLOATS = IC * H * XROW;
-  static constexpr int EPI_ROWS = NW * LS * TT;             // transforms per epilogue round
+  static constexpr int EPI_ROWS = NW * LS * TT;
   static constexpr int EPI_FLOATS = EPI_ROWS * SROW;
   static constexpr int MAIN_FLOATS = STAGE_FLOATS + XF_FLOATS;
-  static constexpr int LDS_FLOATS =
-      MAIN_OFF + (MAIN_FLOATS > EPI_FLOATS ? MAIN_FLOATS : EPI_FLOATS);
+  static constexpr int LDS_FLOATS = MAIN_OFF + (MAIN_FLOATS > EPI_FLOATS ? MAIN_FLOATS : EPI_FLOATS);
   static_assert(NGROUPS % TT == 0, "FFT groups must cover whole token columns");
   static_assert(EPI_ROWS % NGROUPS == 0, "epilogue rows per group");
   static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
   static_assert(BPL * OPL * TT * 2 == 128, "accumulator budget");
 };
 
-template <int XT> struct XTraits;
-template <> struct XTraits<BCFFT_F32> { static constexpr int ES = 4; };
-template <> struct XTraits<BCFFT_F16> { static constexpr int ES = 2; };
-template <> struct XTraits<BCFFT_BF16> { static constexpr int ES = 2; };
-
-// ------------------------------------------------------------------ forward kernel
 template <int B, int XT>
-__global__ __launch_bounds__(512) void bc_forward_kernel(
+__global__ __launch_bounds__(512) void bc_forward_valu_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_in, int n_out,
     const float2* __restrict__ spec, const void* __restrict__ bias, int bias_dt,
     void* __restrict__ yv, int y_dt) {
-  using G = Geo<B>;
-  constexpr int H = G::H, L = G::L, P = G::P, Q = G::Q, TT = G::TT, IC = G::IC;
-  constexpr int SROW = G::SROW, XROW = G::XROW;
-  constexpr int VEC = 16 / XTraits<XT>::ES;             // elements per 16 B load
+  using G = GeoV<B>;
+  using F = Fft<B>;
+  constexpr int H = G::H, L = G::L, TT = G::TT, IC = G::IC, SROW = G::SROW, XROW = G::XROW;
+  constexpr int VEC = 16 / XTraits<XT>::ES;
   constexpr int CHUNK_ELEMS = TT * IC * B;
-  constexpr int NLD = CHUNK_ELEMS / (G::NT * VEC);     // 16 B loads per thread per chunk
+  constexpr int NLD = CHUNK_ELEMS / (G::NT * VEC);
   static_assert(CHUNK_ELEMS % (G::NT * VEC) == 0, "chunk/loader mismatch");
 
   __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
-  float2* tw = reinterpret_cast<float2*>(lds + G::TW_OFF);   // W_b^m = exp(-2 pi i m / b)
+  float2* tw = reinterpret_cast<float2*>(lds);
   float* stage = lds + G::MAIN_OFF;
   float* xf = lds + G::XF_OFF;
 
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
   const int64_t t0 = (int64_t)blockIdx.x * TT;
   const int o_base = blockIdx.y * G::OUT_PER_WG;
   const int K = n_in * B;
   const int64_t M = (int64_t)n_out * B;
 
-  // twiddle table (stored by bcfft_spectra after the packed bins)
-  const float2* twg = spec + (int64_t)n_out * n_in * H;
+  const float2* twg = spec + spec_layout(n_out, n_in, B).tw_off_f2;
   for (int m = tid; m < B; m += G::NT) tw[m] = twg[m];
 
-  // ---- FFT group identity: group g = il*TT + t handles (token t, chunk block il)
-  const int g = tid / L;
-  const int gl = tid % L;                 // lane within the FFT group
-  const int g_t = g % TT;
-  const int g_il = g / TT;
-
-  // ---- CMAC identity
+  const int g = tid / L, gl = tid % L;    // FFT group (token g % TT, chunk block g / TT)
+  const int g_t = g % TT, g_il = g / TT;
   const int lb = lane % G::LBINS;         // first bin of this lane
   const int ls = lane / G::LBINS;         // output sub-group
-  const int o_lane = o_base + (wave * G::LS + ls) * G::OPL;   // first output of this lane
+  const int o_lane = o_base + (wave * G::LS + ls) * G::OPL;
   const bool wave_active = (o_base + wave * G::LS * G::OPL) < n_out;
 
   float acc[G::BPL][G::OPL][TT][2];
@@ -223,136 +399,62 @@ __global__ __launch_bounds__(512) void bc_forward_kernel(
 #pragma unroll
       for (int t = 0; t < TT; ++t) acc[j][q][t][0] = acc[j][q][t][1] = 0.f;
 
-  // ---- chunk loader (x -> registers, prefetched one chunk ahead)
   uint4 xr[NLD];
   auto load_chunk = [&](int i0) {
 #pragma unroll
     for (int u = 0; u < NLD; ++u) {
       const int e = (u * G::NT + tid) * VEC;
-      const int t = e / (IC * B);
-      const int r = e % (IC * B);
-      const int il = r / B;
-      const int pos = r % B;
+      const int t = e / (IC * B), r = e % (IC * B), il = r / B, pos = r % B;
       const int64_t tok = t0 + t;
-      if (tok < n_tokens && i0 + il < n_in) {
-        const char* src = (const char*)xv +
-                          ((tok * K + (int64_t)(i0 + il) * B + pos) * XTraits<XT>::ES);
-        xr[u] = *reinterpret_cast<const uint4*>(src);
-      } else {
-        xr[u] = make_uint4(0, 0, 0, 0);
-      }
+      xr[u] = (tok < n_tokens && i0 + il < n_in)
+                  ? *reinterpret_cast<const uint4*>((const char*)xv +
+                        ((tok * K + (int64_t)(i0 + il) * B + pos) * XTraits<XT>::ES))
+                  : make_uint4(0, 0, 0, 0);
     }
   };
   auto store_chunk = [&]() {
 #pragma unroll
     for (int u = 0; u < NLD; ++u) {
       const int e = (u * G::NT + tid) * VEC;
-      const int t = e / (IC * B);
-      const int r = e % (IC * B);
-      const int il = r / B;
-      const int pos = r % B;
-      float* dst = stage + (il * TT + t) * SROW + pos;
-      if constexpr (XT == BCFFT_F32) {
-        *reinterpret_cast<uint4*>(dst) = xr[u];
-      } else {
-        const uint32_t w[4] = {xr[u].x, xr[u].y, xr[u].z, xr[u].w};
-        float f[8];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if constexpr (XT == BCFFT_BF16) {
-            f[2 * k] = bf16_to_f32(w[k] & 0xffffu);
-            f[2 * k + 1] = bf16_to_f32(w[k] >> 16);
-          } else {
-            f[2 * k] = f16_to_f32(w[k] & 0xffffu);
-            f[2 * k + 1] = f16_to_f32(w[k] >> 16);
-          }
-        }
-        *reinterpret_cast<float4*>(dst) = make_float4(f[0], f[1], f[2], f[3]);
-        *reinterpret_cast<float4*>(dst + 4) = make_float4(f[4], f[5], f[6], f[7]);
-      }
+      const int t = e / (IC * B), r = e % (IC * B), il = r / B, pos = r % B;
+      stage_store<XT>(stage + (il * TT + t) * SROW + pos, xr[u]);
     }
   };
-
-  // ---- spectra coefficient loads for one input block (o-major, bins contiguous)
   auto load_coef = [&](int i, float2 (&c)[G::BPL][G::OPL]) {
 #pragma unroll
     for (int j = 0; j < G::BPL; ++j)
 #pragma unroll
       for (int q = 0; q < G::OPL; ++q) {
         const int o = o_lane + q;
-        c[j][q] = (o < n_out && i < n_in)
-                      ? spec[((int64_t)o * n_in + i) * H + lb + G::LBINS * j]
-                      : make_float2(0.f, 0.f);
+        c[j][q] = (o < n_out && i < n_in) ? spec[((int64_t)o * n_in + i) * H + lb + G::LBINS * j]
+                                          : make_float2(0.f, 0.f);
       }
   };
 
   const int n_chunks = (n_in + IC - 1) / IC;
   load_chunk(0);
-  __syncthreads();  // twiddles visible
+  __syncthreads();
 
   for (int ch = 0; ch < n_chunks; ++ch) {
     const int i0 = ch * IC;
-    __syncthreads();  // previous chunk's CMAC is done with xf / stage
+    __syncthreads();
     store_chunk();
     float2 cbuf[2][G::BPL][G::OPL];
     if (wave_active) load_coef(i0, cbuf[0]);
     __syncthreads();
-
-    // ================= forward real FFT of row g (token g_t, block i0+g_il)
     {
       float* row = stage + g * SROW;
-      float2 v[P];
-#pragma unroll
-      for (int n2 = 0; n2 < P; ++n2)
-        v[n2] = *reinterpret_cast<const float2*>(row + 2 * (gl + L * n2));
-      dft<P, false>(v);
-#pragma unroll
-      for (int k2 = 1; k2 < P; ++k2) v[k2] = cmul(v[k2], tw[(2 * gl * k2) % B]);   // W_H^(n1 k2)
-      wave_lds_sync();
-#pragma unroll
-      for (int k2 = 0; k2 < P; ++k2)
-        *reinterpret_cast<float2*>(row + 2 * (k2 * (L + 1) + gl)) = v[k2];
-      wave_lds_sync();
-      float2 u[Q][L];
-#pragma unroll
-      for (int m = 0; m < Q; ++m)
-#pragma unroll
-        for (int n1 = 0; n1 < L; ++n1)
-          u[m][n1] = *reinterpret_cast<const float2*>(row + 2 * ((gl + L * m) * (L + 1) + n1));
-#pragma unroll
-      for (int m = 0; m < Q; ++m) dft<L, false>(u[m]);
-      wave_lds_sync();
-#pragma unroll
-      for (int m = 0; m < Q; ++m)
-#pragma unroll
-        for (int k1 = 0; k1 < L; ++k1)   // Z[P*k1 + k2], k2 = gl + L*m, natural order
-          *reinterpret_cast<float2*>(row + 2 * (P * k1 + gl + L * m)) = u[m][k1];
-      wave_lds_sync();
-      // untangle: X'[k] = (Zk + Zm) - i W_b^k (Zk - Zm), Zm = conj(Z[H-k]); k = gl + L*jj
+      F::template forward<BCFFT_F32>(row, gl, tw);
       float* xdst = xf + (g_il * H) * XROW + 2 * g_t;
 #pragma unroll
-      for (int jj = 0; jj < P; ++jj) {
+      for (int jj = 0; jj < F::P; ++jj) {
         const int k = gl + L * jj;
-        const float2 zk = *reinterpret_cast<const float2*>(row + 2 * k);
-        const float2 zh = *reinterpret_cast<const float2*>(row + 2 * ((H - k) & (H - 1)));
-        const float sr = zk.x + zh.x, si = zk.y - zh.y;   // Zk + conj(Z[H-k])
-        const float dr = zk.x - zh.x, di = zk.y + zh.y;   // Zk - conj(Z[H-k])
-        const float2 w = tw[k];
-        float2 o;
-        o.x = sr + w.x * di + w.y * dr;
-        o.y = si - w.x * dr + w.y * di;
-        if (jj == 0 && gl == 0) {   // packed bin 0: (2(ReZ0+ImZ0), 2(ReZ0-ImZ0))
-          o.x = 2.f * (zk.x + zk.y);
-          o.y = 2.f * (zk.x - zk.y);
-        }
-        *reinterpret_cast<float2*>(xdst + k * XROW) = o;
+        *reinterpret_cast<float2*>(xdst + k * XROW) = F::untangle(row, k, tw);
       }
     }
-    // prefetch the next chunk behind the CMAC (live only during the CMAC)
     if (ch + 1 < n_chunks) load_chunk(i0 + IC);
     __syncthreads();
 
-    // ================= CMAC: acc[bin][out][tok] += S[out][i][bin] * X'[tok][i][bin]
     if (wave_active) {
 #pragma unroll
       for (int il = 0; il < IC; ++il) {
@@ -395,12 +497,10 @@ __global__ __launch_bounds__(512) void bc_forward_kernel(
     }
   }
 
-  // ================= epilogue: inverse real FFT per (output, token), + bias, store
-  constexpr int TPG = G::EPI_ROWS / G::NGROUPS;    // transforms per FFT group per round
+  constexpr int TPG = G::EPI_ROWS / G::NGROUPS;
 #pragma unroll
   for (int q = 0; q < G::OPL; ++q) {
-    __syncthreads();   // previous round (or the last CMAC) is done with the LDS
-    // rows: R = (wave*LS + ls)*TT + t, complex index = bin
+    __syncthreads();
 #pragma unroll
     for (int j = 0; j < G::BPL; ++j)
 #pragma unroll
@@ -413,94 +513,252 @@ __global__ __launch_bounds__(512) void bc_forward_kernel(
 #pragma unroll 1
     for (int u2 = 0; u2 < TPG; ++u2) {
       const int R = g + G::NGROUPS * u2;
-      const int sub = R / TT;                // = wave*LS + ls of the writer
       const int t = R % TT;
-      const int o = o_base + sub * G::OPL + q;
+      const int o = o_base + (R / TT) * G::OPL + q;
       float* row = stage + R * SROW;
-      // pre-process + step-1 load: Zi[k] = E + iO, E = Y[k] + conj(Y[H-k]),
-      // O = (Y[k] - conj(Y[H-k])) W_b^-k; k = gl + L*n2
-      float2 v[P];
-#pragma unroll
-      for (int n2 = 0; n2 < P; ++n2) {
-        const int k = gl + L * n2;
-        const float2 yk = *reinterpret_cast<const float2*>(row + 2 * k);
-        const float2 yh = *reinterpret_cast<const float2*>(row + 2 * ((H - k) & (H - 1)));
-        const float er = yk.x + yh.x, ei = yk.y - yh.y;
-        const float dr = yk.x - yh.x, di = yk.y + yh.y;
-        const float2 w = tw[k];                       // use conj(w)
-        float2 z;
-        z.x = er - (di * w.x - dr * w.y);
-        z.y = ei + (dr * w.x + di * w.y);
-        if (n2 == 0 && gl == 0) {   // packed bin 0: (Y0 + YH) + i (Y0 - YH)
-          z.x = yk.x + yk.y;
-          z.y = yk.x - yk.y;
-        }
-        v[n2] = z;
-      }
-      dft<P, true>(v);
-#pragma unroll
-      for (int k2 = 1; k2 < P; ++k2) v[k2] = cmulc(v[k2], tw[(2 * gl * k2) % B]);
-      wave_lds_sync();
-#pragma unroll
-      for (int k2 = 0; k2 < P; ++k2)
-        *reinterpret_cast<float2*>(row + 2 * (k2 * (L + 1) + gl)) = v[k2];
-      wave_lds_sync();
-      float2 uu[Q][L];
-#pragma unroll
-      for (int m = 0; m < Q; ++m)
-#pragma unroll
-        for (int n1 = 0; n1 < L; ++n1)
-          uu[m][n1] = *reinterpret_cast<const float2*>(row + 2 * ((gl + L * m) * (L + 1) + n1));
-#pragma unroll
-      for (int m = 0; m < Q; ++m) dft<L, true>(uu[m]);
-      wave_lds_sync();
-#pragma unroll
-      for (int m = 0; m < Q; ++m)
-#pragma unroll
-        for (int k1 = 0; k1 < L; ++k1)   // z[m'] = (y[2m'], y[2m'+1]), m' = P*k1 + k2
-          *reinterpret_cast<float2*>(row + 2 * (P * k1 + gl + L * m)) = uu[m][k1];
-      wave_lds_sync();
-      // store: lane gl writes float4 pieces gl, gl+L, ... of the b outputs
+      F::inverse(row, gl, tw, 0);
       const int64_t tok = t0 + t;
-      if (tok < n_tokens && o < n_out) {
-#pragma unroll
-        for (int pc = 0; pc < B / (4 * L); ++pc) {
-          const int p4 = (gl + L * pc) * 4;
-          float4 val = *reinterpret_cast<const float4*>(row + p4);
-          float vv[4] = {val.x, val.y, val.z, val.w};
-          const int64_t col = (int64_t)o * B + p4;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float r = round_to(vv[e], XT);                  // y32.to(x.dtype)  (:266)
-            if (bias_dt != BCFFT_NONE) r += load_scalar(bias, col + e, bias_dt);  // (:270-271)
-            vv[e] = r;
-          }
-          const int64_t off = tok * M + col;
-          if (y_dt == BCFFT_F32) {
-            *reinterpret_cast<float4*>((float*)yv + off) = make_float4(vv[0], vv[1], vv[2], vv[3]);
-          } else {
-            uint32_t h[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) h[e] = y_dt == BCFFT_BF16 ? f32_to_bf16(vv[e]) : f32_to_f16(vv[e]);
-            *reinterpret_cast<uint2*>((uint16_t*)yv + off) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
-          }
-        }
-      }
+      if (tok < n_tokens && o < n_out)
+        F::template store<XT>(row, gl, yv, tok * M + (int64_t)o * B, bias, (int64_t)o * B, bias_dt, y_dt);
     }
   }
 }
 
-// ------------------------------------------------------------------ spectra kernel
-// One thread per packed bin: direct DFT of the b-point column in fp64, scaled 1/(2b).
+// ================================================================== MFMA forward kernel
+// CMAC per bin f as a real GEMM on v_mfma_f32_16x16x32_bf16:
+//   rows (M=16) = 8 tokens x {re, im} of the output, cols (N=16) = 16 output blocks,
+//   K = 32 = {X hi, X lo} x 8 input blocks x {re, im} of the input.
+//   A[(t,re)][(i,*)] = (xr, xi), A[(t,im)][(i,*)] = (xi, -xr), B[(i,*)][o] = conj(C[o,i])
+//   => D[(t,re)][o] = sum_i Re(C X), D[(t,im)][o] = sum_i Im(C X).
+//   Bin 0 (packed DC/Nyquist, both real): A = (X0, 0) / (0, X_H), B = (C0, C_H).
+//   Two MFMAs per tile: B = C_hi and B = C_lo -> (Xhi + Xlo)(Chi + Clo), fp32 accumulate.
+template <int B>
+struct GeoM {
+  using F = Fft<B>;
+  static constexpr int H = B / 2, L = F::L, SROW = F::SROW;
+  static constexpr int TT = 8, NW = 4, NT = NW * 64;   // 8 tokens = one MFMA row tile
+  static constexpr int KB = 8;                    // input blocks per chunk (MFMA K = 32)
+  static constexpr int BPW = H / NW;              // bins per wave
+  static constexpr int NTL = 32 / BPW;            // 16-output N-tiles per workgroup
+  static constexpr int OUT_PER_WG = 16 * NTL;
+  static constexpr int NGROUPS = NT / L;
+  static constexpr int ROWS = TT * KB;            // transforms per chunk
+  static constexpr int TPC = ROWS / NGROUPS;      // transforms per FFT group per chunk
+  static constexpr int XS = 2 * TT * KB + 4;      // dwords per bin of the split-X image (+4 pad)
+  static constexpr int MAIN_OFF = 2 * B;
+  static constexpr int STAGE_FLOATS = ROWS * SROW;
+  static constexpr int XL_OFF = MAIN_OFF + STAGE_FLOATS;
+  static constexpr int XL_FLOATS = H * XS;
+  static constexpr int EPI_ROWS = 16 * TT;        // one N-tile: 16 outputs x TT tokens
+  static constexpr int EPI_FLOATS = EPI_ROWS * SROW;
+  static constexpr int MAIN_FLOATS = STAGE_FLOATS + XL_FLOATS;
+  static constexpr int LDS_FLOATS = MAIN_OFF + (MAIN_FLOATS > EPI_FLOATS ? MAIN_FLOATS : EPI_FLOATS);
+  static constexpr int STEPS = BPW * NTL;         // (bin, N-tile) steps per wave per chunk
+  static constexpr int RING = 4;                  // B-fragment prefetch depth (steps)
+
+  static_assert(BPW * NTL * 4 == 128, "accumulator budget");
+  static_assert(ROWS % NGROUPS == 0 && EPI_ROWS % NGROUPS == 0, "group tiling");
+  static_assert(H >= 16, "bin swizzle needs H >= 16");
+  static_assert(LDS_FLOATS * 4 <= 80 * 1024, "LDS budget: two workgroups per CU");
+};
+
+template <int B, int XT>
+__global__ __launch_bounds__(256, 2) void bc_forward_mfma_kernel(
+    const void* __restrict__ xv, int64_t n_tokens, int n_in, int n_out,
+    const float2* __restrict__ spec, const void* __restrict__ bias, int bias_dt,
+    void* __restrict__ yv, int y_dt, int dbg) {
+  using G = GeoM<B>;
+  using F = Fft<B>;
+  constexpr int H = G::H, L = G::L, TT = G::TT, KB = G::KB, SROW = G::SROW, XS = G::XS;
+  constexpr int NTL = G::NTL, BPW = G::BPW, STEPS = G::STEPS, RING = G::RING;
+
+    __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
+  float2* tw = reinterpret_cast<float2*>(lds);
+  float* stage = lds + G::MAIN_OFF;
+  uint32_t* xl = reinterpret_cast<uint32_t*>(lds + G::XL_OFF);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
+  const int64_t t0 = (int64_t)blockIdx.x * TT;
+  const int o_base = blockIdx.y * G::OUT_PER_WG;
+  const int K = n_in * B;
+  const int64_t M = (int64_t)n_out * B;
+
+  const SpecLayout sl = spec_layout(n_out, n_in, B);
+  const float2* twg = spec + sl.tw_off_f2;
+  const uint32_t* img = reinterpret_cast<const uint32_t*>(spec) + sl.img_off_u32;
+  const int64_t prec_stride = (int64_t)sl.n_out_pad * 8;      // dwords between hi and lo slabs
+  for (int m = tid; m < B; m += G::NT) tw[m] = twg[m];
+
+  const int g = tid / L, gl = tid % L;    // FFT group
+  // MFMA lane roles
+  const int row = lane & 15, kb = lane >> 4;
+  const int a_prec = kb >> 1, a_half = kb & 1;
+  const int p_out = row & 1;
+  const uint32_t a_sel = p_out ? 0x01000302u : 0x03020100u;   // im rows: swap (xr, xi)
+  const uint32_t a_xor = p_out ? 0x80000000u : 0u;            //   -> (xi, -xr)
+  const uint32_t a_bin0 = p_out ? 0xffff0000u : 0x0000ffffu;  // bin 0: (X0, 0) / (0, X_H)
+
+  f32x4 acc[BPW][NTL];
+#pragma unroll
+  for (int fb = 0; fb < BPW; ++fb)
+#pragma unroll
+    for (int nt = 0; nt < NTL; ++nt) acc[fb][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // x chunk -> LDS rows by LDS-DMA (raw dtype, row T = token*KB + block). One wave
+  // instruction moves 64 lanes x DS bytes of one row; rows stay padded to SROW floats.
+  auto dma_chunk = [&](int i0) {
+    constexpr int ES = XTraits<XT>::ES;
+    constexpr int ROW_BYTES = B * ES;
+    // LDS-DMA writes lane l's dword at base + 4l (also for sub-dword sizes), so rows shorter
+    // than 256 B use dword DMA with ROW_BYTES/4 active lanes
+    constexpr int IPR = ROW_BYTES >= 256 ? ROW_BYTES / 256 : 1;     // instructions per row
+    constexpr int ACTIVE = ROW_BYTES >= 256 ? 64 : ROW_BYTES / 4;    // lanes per instruction
+    constexpr int NINST = G::ROWS * IPR;
+    static_assert(NINST % G::NW == 0, "DMA instructions per wave");
+#pragma unroll 1
+    for (int q0 = 0; q0 < NINST / G::NW; ++q0) {   // a real loop: keeps addresses out of VGPRs
+      const int q = q0 * G::NW + wave;
+      const int T = q / IPR, piece = q % IPR;
+      const int t = T / KB, blk = T % KB;
+      const int64_t tok = t0 + t;
+      char* dst = reinterpret_cast<char*>(stage + T * SROW) + piece * 256;
+      if (lane < ACTIVE) {
+        if (tok < n_tokens && i0 + blk < n_in) {
+          const char* src = (const char*)xv + (tok * K + (int64_t)(i0 + blk) * B) * ES + piece * 256 + lane * 4;
+          if (dbg & 32)     // debug: plain load + ds_write instead of LDS-DMA
+            reinterpret_cast<uint32_t*>(dst)[lane] = *reinterpret_cast<const uint32_t*>(src);
+          else
+          __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                           (__attribute__((address_space(3))) void*)dst, 4, 0, 0);
+        } else {                                  // zero-fill rows past the end (no NaN garbage)
+          reinterpret_cast<uint32_t*>(dst)[lane] = 0u;
+        }
+      }
+    }
+  };
+  // B fragments (hi, lo) for step s of chunk c: 16 B each, 8 blocks of output o
+  auto load_b = [&](int c, int s, uint4 (&dst)[2]) {
+    const int fb = s / NTL, nt = s % NTL;
+    const int f = wave * BPW + fb;
+    const int o = o_base + 16 * nt + row;
+    const uint32_t* p = img + ((int64_t)(c * H + f) * 2) * prec_stride + o * 8 + a_half * 4;
+    dst[0] = *reinterpret_cast<const uint4*>(p);
+    dst[1] = *reinterpret_cast<const uint4*>(p + prec_stride);
+  };
+
+  const int n_chunks = sl.n_chunk;
+  if (!(dbg & 16)) dma_chunk(0);
+
+  for (int ch = 0; ch < n_chunks; ++ch) {
+    const int i0 = ch * KB;
+    __syncthreads();   // x chunk landed (the barrier waits vmcnt(0)); MFMA phase done with xl
+    if ((dbg & 256) && ch == (dbg >> 16)) {   // debug: dump the staged x rows into y, stop
+      for (int i = tid; i < G::STAGE_FLOATS; i += G::NT) ((float*)yv)[t0 * M + i] = stage[i];
+      return;
+    }
+    uint4 bring[RING][2];
+#pragma unroll
+    for (int s = 0; s < RING; ++s) load_b(ch, s, bring[s]);
+    __syncthreads();
+
+    // ---- forward FFTs: transform T = g + NGROUPS*u -> (token T / KB, block T % KB)
+#pragma unroll 1
+    for (int u = 0; u < G::TPC; ++u) {
+      const int T = g + G::NGROUPS * u;
+      float* rowp = stage + T * SROW;
+      if (!(dbg & 4)) F::template forward<XT>(rowp, gl, tw);
+      uint32_t* dst = xl + (T / KB) * KB + (T % KB);
+#pragma unroll
+      for (int jj = 0; jj < F::P; ++jj) {
+        const int k = gl + L * jj;
+        uint32_t hi, lo;
+        split_bf16(F::untangle(rowp, k, tw), hi, lo);
+        dst[k * XS] = hi;                    // [bin][prec][token][block]
+        dst[k * XS + TT * KB] = lo;
+      }
+    }
+    __syncthreads();
+    if ((dbg & 128) && ch == (dbg >> 16)) {   // debug: dump the split-X image into y, stop
+      for (int i = tid; i < G::XL_FLOATS; i += G::NT) ((uint32_t*)yv)[t0 * M + i] = xl[i];
+      return;
+    }
+    if (ch + 1 < n_chunks && !(dbg & 16)) dma_chunk(i0 + KB);    // next x chunk behind the MFMAs
+
+    // ---- MFMA complex MAC over the chunk's 8 blocks
+    uint4 afrag;
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s) {
+      const int fb = s / NTL, nt = s % NTL;
+      const int f = wave * BPW + fb;
+      if (nt == 0) {
+        const int t = row >> 1;
+        uint4 raw = *reinterpret_cast<const uint4*>(xl + f * XS + (a_prec * TT + t) * KB + a_half * 4);
+        if (f == 0) {
+          raw.x &= a_bin0; raw.y &= a_bin0; raw.z &= a_bin0; raw.w &= a_bin0;
+        } else {
+          raw.x = __builtin_amdgcn_perm(raw.x, raw.x, a_sel) ^ a_xor;
+          raw.y = __builtin_amdgcn_perm(raw.y, raw.y, a_sel) ^ a_xor;
+          raw.z = __builtin_amdgcn_perm(raw.z, raw.z, a_sel) ^ a_xor;
+          raw.w = __builtin_amdgcn_perm(raw.w, raw.w, a_sel) ^ a_xor;
+        }
+        afrag = raw;
+      }
+      uint4 bcur[2] = {bring[s % RING][0], bring[s % RING][1]};
+      if (s + RING < STEPS && !(dbg & 2)) load_b(ch, s + RING, bring[s % RING]);
+      if (dbg & 1) {   // ablation: keep the operands live, skip the MFMAs
+        asm volatile("" :: "v"(bcur[0].x), "v"(bcur[1].x), "v"(afrag.x));
+        continue;
+      }
+      const bf16x8 a = __builtin_bit_cast(bf16x8, afrag);
+      acc[fb][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, bcur[0]), acc[fb][nt], 0, 0, 0);
+      acc[fb][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, bcur[1]), acc[fb][nt], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue, one 16-output N-tile per round. D layout: col = lane & 15 (output),
+  //      row = 4*(lane >> 4) + r -> token 2*(lane >> 4) + (r >> 1), part r & 1.
+  //      LDS row R = o_local*TT + t holds bin f at complex column f ^ o_local (bank spread).
+#pragma unroll
+  for (int nt = 0; nt < NTL; ++nt) {
+    __syncthreads();
+#pragma unroll
+    for (int fb = 0; fb < BPW; ++fb) {
+      const int f = wave * BPW + fb;
+      const int R = row * TT + 2 * kb;
+      const f32x4 a = acc[fb][nt];
+      float* p = stage + R * SROW + 2 * (f ^ row);
+      *reinterpret_cast<float2*>(p) = make_float2(a[0], a[1]);
+      *reinterpret_cast<float2*>(p + SROW) = make_float2(a[2], a[3]);
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int u2 = 0; u2 < G::EPI_ROWS / G::NGROUPS; ++u2) {
+      const int R = g + G::NGROUPS * u2;
+      const int ol = R / TT, t = R % TT;
+      const int o = o_base + 16 * nt + ol;
+      float* rowp = stage + R * SROW;
+      if (!(dbg & 8)) F::inverse(rowp, gl, tw, ol);
+      const int64_t tok = t0 + t;
+      if (tok < n_tokens && o < n_out)
+        F::template store<XT>(rowp, gl, yv, tok * M + (int64_t)o * B, bias, (int64_t)o * B, bias_dt, y_dt);
+    }
+  }
+}
+
+// ================================================================== spectra kernels
+// Packed spectra of the OPERATOR (n_out x n_in blocks; transpose_conj: the adjoint built
+// from c's (n_in x n_out) grid): one thread per packed bin, direct DFT in fp64, 1/(2b).
 template <int B>
 __global__ void bc_spectra_kernel(const void* __restrict__ c, int c_dt, int n_out, int n_in,
                                   int transpose_conj, float2* __restrict__ spec) {
   constexpr int H = B / 2;
-  const int64_t blk = blockIdx.x;            // (o, i) pair
-  const int k = threadIdx.x;                 // packed bin
+  const int64_t blk = blockIdx.x;            // operator (o, i) pair
+  const int k = threadIdx.x;
   if (blk < (int64_t)n_out * n_in && k < H) {
     const int o = (int)(blk / n_in), i = (int)(blk % n_in);
-    const int64_t base = blk * B;
+    // c is (n_out, n_in, B) for the plain operator and (n_in, n_out, B) for the adjoint
+    const int64_t base = (transpose_conj ? ((int64_t)i * n_out + o) : blk) * B;
     double re = 0.0, im = 0.0, re_h = 0.0;
     for (int n = 0; n < B; ++n) {
       const double v = (double)load_scalar(c, base + n, c_dt);
@@ -514,19 +772,47 @@ __global__ void bc_spectra_kernel(const void* __restrict__ c, int c_dt, int n_ou
     float2 out;
     if (k == 0) out = make_float2((float)(re * sc), (float)(re_h * sc));
     else out = make_float2((float)(re * sc), (float)((transpose_conj ? -im : im) * sc));
-    const int64_t dst = transpose_conj ? ((int64_t)i * n_out + o) : ((int64_t)o * n_in + i);
-    spec[dst * H + k] = out;
+    spec[blk * H + k] = out;
   }
-  if (blk == 0) {   // twiddle table W_b^m, m < b
+  if (blk == 0) {
+    const int64_t tw_off = spec_layout(n_out, n_in, B).tw_off_f2;
     for (int m = threadIdx.x; m < B; m += blockDim.x) {
       double s, co;
       sincospi(2.0 * (double)m / (double)B, &s, &co);
-      spec[(int64_t)n_out * n_in * H + m] = make_float2((float)co, (float)(-s));
+      spec[tw_off + m] = make_float2((float)co, (float)(-s));
     }
   }
 }
 
-// ------------------------------------------------------------------ circulant matvec
+// MFMA image from the packed spectra (one thread per image dword pair hi/lo)
+template <int B>
+__global__ void bc_mfma_image_kernel(int n_out, int n_in, float2* __restrict__ spec) {
+  constexpr int H = B / 2;
+  const SpecLayout sl = spec_layout(n_out, n_in, B);
+  uint32_t* img = reinterpret_cast<uint32_t*>(spec) + sl.img_off_u32;
+  const int64_t per_prec = (int64_t)sl.n_out_pad * 8;
+  const int64_t total = (int64_t)sl.n_chunk * H * per_prec;   // (c, f, o, j) quadruples
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(idx & 7);
+    const int o = (int)((idx >> 3) % sl.n_out_pad);
+    const int64_t cf = (idx >> 3) / sl.n_out_pad;
+    const int f = (int)(cf % H), c = (int)(cf / H);
+    const int i = 8 * c + j;
+    float2 v = make_float2(0.f, 0.f);
+    if (o < n_out && i < n_in) {
+      v = spec[((int64_t)o * n_in + i) * H + f];
+      if (f != 0) v.y = -v.y;                 // conj(C); bin 0 keeps (C0, C_H)
+    }
+    uint32_t hi, lo;
+    split_bf16(v, hi, lo);
+    const int64_t d = ((int64_t)(c * H + f) * 2) * per_prec + (int64_t)o * 8 + j;
+    img[d] = hi;
+    img[d + per_prec] = lo;
+  }
+}
+
+// ================================================================== circulant matvec
 __global__ void circulant_matvec_kernel(const void* __restrict__ c, const void* __restrict__ x,
                                         int dt, int n, void* __restrict__ y) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -560,22 +846,55 @@ bool valid_dt(int d) { return d == BCFFT_F32 || d == BCFFT_F16 || d == BCFFT_BF1
 bool valid_block(int b) { return b == 32 || b == 64 || b == 128 || b == 256; }
 int promote(int a, int b) { return (b == BCFFT_NONE || a == b) ? a : BCFFT_F32; }
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+// Analysis switches (BCFFT_DEBUG_FLAGS; results are WRONG when set; production never sets it):
+// ablation: 1 skip MFMAs, 2 skip B-fragment loads, 4 skip forward FFT math, 8 skip inverse FFT
+// math, 16 skip x prefetch loads, 32 plain loads instead of LDS-DMA, 64 force one workgroup
+// per CU; LDS dumps (chunk = flags >> 16, written into the tile's y rows, then return):
+// 128 split-X image after the FFT phase, 256 staged x rows after the load (tools/dump_check.py).
+int debug_flags() {
+  const char* e = getenv("BCFFT_DEBUG_FLAGS");
+  return e ? atoi(e) : 0;
+}
 
 template <int B, int XT>
-void launch_forward(const void* x, int64_t n, int n_in, int n_out, const void* spec,
+void launch_forward(int algo, const void* x, int64_t n, int n_in, int n_out, const void* spec,
                     const void* bias, int bias_dt, void* y, int y_dt, hipStream_t s) {
-  using G = bcfft::Geo<B>;
+  if constexpr (B <= 128) {
+    if (algo == BCFFT_ALGO_MFMA) {
+      using G = bcfft::GeoM<B>;
+      dim3 grid((unsigned)((n + G::TT - 1) / G::TT), (unsigned)((n_out + G::OUT_PER_WG - 1) / G::OUT_PER_WG));
+      const int dbg = debug_flags();   // 64: pad dynamic LDS to force one workgroup per CU
+      hipLaunchKernelGGL((bcfft::bc_forward_mfma_kernel<B, XT>), grid, dim3(G::NT), (dbg & 64) ? 65536 : 0, s, x, n,
+                         n_in, n_out, (const float2*)spec, bias, bias_dt, y, y_dt, dbg);
+      return;
+    }
+  }
+  using G = bcfft::GeoV<B>;
   dim3 grid((unsigned)((n + G::TT - 1) / G::TT), (unsigned)((n_out + G::OUT_PER_WG - 1) / G::OUT_PER_WG));
-  hipLaunchKernelGGL((bcfft::bc_forward_kernel<B, XT>), grid, dim3(G::NT), 0, s, x, n, n_in,
+  hipLaunchKernelGGL((bcfft::bc_forward_valu_kernel<B, XT>), grid, dim3(G::NT), 0, s, x, n, n_in,
                      n_out, (const float2*)spec, bias, bias_dt, y, y_dt);
 }
 
 template <int B>
-void launch_forward_b(int xdt, const void* x, int64_t n, int n_in, int n_out, const void* spec,
-                      const void* bias, int bias_dt, void* y, int y_dt, hipStream_t s) {
-  if (xdt == BCFFT_F32) launch_forward<B, BCFFT_F32>(x, n, n_in, n_out, spec, bias, bias_dt, y, y_dt, s);
-  else if (xdt == BCFFT_F16) launch_forward<B, BCFFT_F16>(x, n, n_in, n_out, spec, bias, bias_dt, y, y_dt, s);
-  else launch_forward<B, BCFFT_BF16>(x, n, n_in, n_out, spec, bias, bias_dt, y, y_dt, s);
+void launch_forward_b(int algo, int xdt, const void* x, int64_t n, int n_in, int n_out,
+                      const void* spec, const void* bias, int bias_dt, void* y, int y_dt, hipStream_t s) {
+  if (xdt == BCFFT_F32) launch_forward<B, BCFFT_F32>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, y_dt, s);
+  else if (xdt == BCFFT_F16) launch_forward<B, BCFFT_F16>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, y_dt, s);
+  else launch_forward<B, BCFFT_BF16>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, y_dt, s);
+}
+
+template <int B>
+void launch_spectra(const void* c, int c_dt, int n_out, int n_in, int tc, float2* out, hipStream_t s) {
+  const unsigned nblk = (unsigned)((int64_t)n_out * n_in);
+  const unsigned threads = (B / 2) < 64 ? 64u : (unsigned)(B / 2);
+  hipLaunchKernelGGL(bcfft::bc_spectra_kernel<B>, dim3(nblk), dim3(threads), 0, s, c, c_dt,
+                     n_out, n_in, tc, out);
+  if constexpr (B <= 128) {
+    const bcfft::SpecLayout sl = bcfft::spec_layout(n_out, n_in, B);
+    const int64_t total = sl.img_u32 / 2;
+    const unsigned blocks = (unsigned)((total + 255) / 256 < 65535 ? (total + 255) / 256 : 65535);
+    hipLaunchKernelGGL(bcfft::bc_mfma_image_kernel<B>, dim3(blocks), dim3(256), 0, s, n_out, n_in, out);
+  }
 }
 }  // namespace
 
@@ -591,7 +910,7 @@ const char* bcfft_status_string(int status) {
     case BCFFT_ERR_DTYPE: return "unsupported dtype or y dtype != promote(x dtype, bias dtype)";
     case BCFFT_ERR_ALIGN: return "x, y and spectra must be 16-byte aligned";
     case BCFFT_ERR_HIP: return "HIP launch failed";
-    case BCFFT_ERR_ARG: return "NULL pointer argument";
+    case BCFFT_ERR_ARG: return "NULL pointer or invalid argument";
     default: return "unknown status";
   }
 }
@@ -600,7 +919,7 @@ const char* bcfft_last_hip_error(void) { return g_last_hip_error; }
 
 int64_t bcfft_spectra_bytes(int n_out_blocks, int n_in_blocks, int block_size) {
   if (n_out_blocks <= 0 || n_in_blocks <= 0 || !valid_block(block_size)) return -1;
-  return ((int64_t)n_out_blocks * n_in_blocks * (block_size / 2) + block_size) * 8;
+  return bcfft::spec_layout(n_out_blocks, n_in_blocks, block_size).total_bytes;
 }
 
 int bcfft_spectra(const void* c, int c_dtype, int n_out_blocks, int n_in_blocks, int block_size,
@@ -611,22 +930,20 @@ int bcfft_spectra(const void* c, int c_dtype, int n_out_blocks, int n_in_blocks,
   if (!valid_dt(c_dtype)) return BCFFT_ERR_DTYPE;
   if (!aligned16(spectra)) return BCFFT_ERR_ALIGN;
   hipStream_t s = (hipStream_t)stream;
-  const unsigned nblk = (unsigned)((int64_t)n_out_blocks * n_in_blocks);
-  const int h = block_size / 2;
-  const unsigned threads = h < 64 ? 64 : (unsigned)h;
   float2* out = (float2*)spectra;
+  const int tc = transpose_conj ? 1 : 0;
   switch (block_size) {
-    case 32: hipLaunchKernelGGL(bcfft::bc_spectra_kernel<32>, dim3(nblk), dim3(threads), 0, s, c, c_dtype, n_out_blocks, n_in_blocks, transpose_conj, out); break;
-    case 64: hipLaunchKernelGGL(bcfft::bc_spectra_kernel<64>, dim3(nblk), dim3(threads), 0, s, c, c_dtype, n_out_blocks, n_in_blocks, transpose_conj, out); break;
-    case 128: hipLaunchKernelGGL(bcfft::bc_spectra_kernel<128>, dim3(nblk), dim3(threads), 0, s, c, c_dtype, n_out_blocks, n_in_blocks, transpose_conj, out); break;
-    default: hipLaunchKernelGGL(bcfft::bc_spectra_kernel<256>, dim3(nblk), dim3(threads), 0, s, c, c_dtype, n_out_blocks, n_in_blocks, transpose_conj, out); break;
+    case 32: launch_spectra<32>(c, c_dtype, n_out_blocks, n_in_blocks, tc, out, s); break;
+    case 64: launch_spectra<64>(c, c_dtype, n_out_blocks, n_in_blocks, tc, out, s); break;
+    case 128: launch_spectra<128>(c, c_dtype, n_out_blocks, n_in_blocks, tc, out, s); break;
+    default: launch_spectra<256>(c, c_dtype, n_out_blocks, n_in_blocks, tc, out, s); break;
   }
   return record_launch();
 }
 
-int bcfft_forward(const void* x, int x_dtype, int64_t n_tokens, int in_features,
-                  int out_features, int block_size, const void* spectra, const void* bias,
-                  int bias_dtype, void* y, int y_dtype, void* stream) {
+int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_features,
+                       int out_features, int block_size, const void* spectra, const void* bias,
+                       int bias_dtype, void* y, int y_dtype, int algo, void* stream) {
   if (!valid_block(block_size)) return BCFFT_ERR_BLOCK;
   if (n_tokens < 0 || in_features <= 0 || out_features <= 0 || in_features % block_size ||
       out_features % block_size)
@@ -635,18 +952,27 @@ int bcfft_forward(const void* x, int x_dtype, int64_t n_tokens, int in_features,
     return BCFFT_ERR_DTYPE;
   if (y_dtype != promote(x_dtype, bias_dtype)) return BCFFT_ERR_DTYPE;
   if ((bias == nullptr) != (bias_dtype == BCFFT_NONE)) return BCFFT_ERR_ARG;
+  if (algo != BCFFT_ALGO_AUTO && algo != BCFFT_ALGO_MFMA && algo != BCFFT_ALGO_VALU) return BCFFT_ERR_ARG;
   if (n_tokens == 0) return BCFFT_OK;
   if (!x || !y || !spectra) return BCFFT_ERR_ARG;
   if (!aligned16(x) || !aligned16(y) || !aligned16(spectra)) return BCFFT_ERR_ALIGN;
   const int n_in = in_features / block_size, n_out = out_features / block_size;
+  if (algo == BCFFT_ALGO_AUTO) algo = block_size <= 128 ? BCFFT_ALGO_MFMA : BCFFT_ALGO_VALU;
   hipStream_t s = (hipStream_t)stream;
   switch (block_size) {
-    case 32: launch_forward_b<32>(x_dtype, x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, y_dtype, s); break;
-    case 64: launch_forward_b<64>(x_dtype, x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, y_dtype, s); break;
-    case 128: launch_forward_b<128>(x_dtype, x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, y_dtype, s); break;
-    default: launch_forward_b<256>(x_dtype, x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, y_dtype, s); break;
+    case 32: launch_forward_b<32>(algo, x_dtype, x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, y_dtype, s); break;
+    case 64: launch_forward_b<64>(algo, x_dtype, x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, y_dtype, s); break;
+    case 128: launch_forward_b<128>(algo, x_dtype, x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, y_dtype, s); break;
+    default: launch_forward_b<256>(algo, x_dtype, x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, y_dtype, s); break;
   }
   return record_launch();
+}
+
+int bcfft_forward(const void* x, int x_dtype, int64_t n_tokens, int in_features,
+                  int out_features, int block_size, const void* spectra, const void* bias,
+                  int bias_dtype, void* y, int y_dtype, void* stream) {
+  return bcfft_forward_algo(x, x_dtype, n_tokens, in_features, out_features, block_size, spectra,
+                            bias, bias_dtype, y, y_dtype, BCFFT_ALGO_AUTO, stream);
 }
 
 int bcfft_circulant_matvec(const void* c, const void* x, int dtype, int n, void* y, void* stream) {

@@ -1,0 +1,20 @@
+#!/bin/bash
+# PMC counter passes (one counter group per rocprofv3 run, --kernel-trace only beside --pmc)
+# usage: tools/pmc.sh TAG K M B IO N   -> gpurun_out/pmc_TAG/<group>/...
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+TAG=$1; shift
+OUT=gpurun_out/pmc_$TAG
+mkdir -p $OUT
+timeout -k 10 120 rocprofv3 -L > $OUT/avail.txt 2>&1 || true
+i=0
+for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+           "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_MFMA" \
+           "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT" \
+           "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  timeout -k 10 180 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $OUT/g$i -o run -- \
+      python3 tools/run_fwd.py "$@" 6 > $OUT/g$i.log 2>&1 || echo "group $i ($grp) failed rc=$?" >> $OUT/failures.txt
+done
+exit 0
