@@ -172,16 +172,15 @@ def main():
 
     gather = None
     if world > 1 and args.allgather:
+        from bcfft.shard import gather_rows
         with torch.inference_mode():
-            y = layer(x)
-            out = torch.empty((world * n, m), dtype=y.dtype, device=dev)
             for _ in range(3):
-                dist.all_gather_into_tensor(out, layer(x))
+                gather_rows(layer(x), world * n)
             barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(args.steps):
-                dist.all_gather_into_tensor(out, layer(x))
+                gather_rows(layer(x), world * n)
             torch.cuda.synchronize()
             barrier()
             g_ms = (time.perf_counter() - t0) * 1e3 / args.steps

@@ -65,6 +65,8 @@ def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, bl
     bias_ptr, bias_code = 0, _lib.BCFFT_NONE
     if bias is not None:
         bias = bias.detach().contiguous()
+        if bias.data_ptr() % 16:                 # the epilogue reads bias with 16-B loads
+            bias = bias.clone()
         bias_ptr, bias_code = bias.data_ptr(), _lib.dtype_code(bias.dtype)
     lib = _lib.load()
     code = _lib.ALGOS[(algo or default_algo()).lower()]

@@ -63,13 +63,56 @@ __device__ __forceinline__ float load_scalar(const void* p, int64_t i, int dt) {
   uint32_t h = ((const uint16_t*)p)[i];
   return dt == BCFFT_BF16 ? bf16_to_f32(h) : f16_to_f32(h);
 }
-// v = hi + lo with hi, lo bf16: returns packed (lo16 = first, hi16 = second) pairs
+// v = hi + lo with hi, lo bf16: returns packed (lo16 = first, hi16 = second) pairs. Internal
+// MFMA operands only, so the hardware RNE conversion (v_cvt_pk_bf16_f32, one instruction per
+// pair) is used; outputs keep the bit-exact software rounding above.
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
 __device__ __forceinline__ void split_bf16(float2 v, uint32_t& hi, uint32_t& lo) {
-  const uint32_t hx = f32_to_bf16(v.x), hy = f32_to_bf16(v.y);
-  const uint32_t lx = f32_to_bf16(v.x - bf16_to_f32(hx)), ly = f32_to_bf16(v.y - bf16_to_f32(hy));
-  hi = hx | (hy << 16);
-  lo = lx | (ly << 16);
+  const bf16x2 h = {(__bf16)v.x, (__bf16)v.y};
+  hi = __builtin_bit_cast(uint32_t, h);
+  const bf16x2 l = {(__bf16)(v.x - __uint_as_float(hi << 16)),
+                    (__bf16)(v.y - __uint_as_float(hi & 0xffff0000u))};
+  lo = __builtin_bit_cast(uint32_t, l);
 }
+
+// ------------------------------------------------------------------ LDS-DMA (inline asm)
+// hipcc neither counts an asm load in its s_waitcnt bookkeeping nor drains it at a barrier, so
+// the x stream stays in flight across compute phases; every wait on it is explicit below.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+// LDS[m0 + 16 * lane] <- 16 B at the lane's global address (m0 = wave-uniform LDS byte address)
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory"); }
+// workgroup rendezvous on LDS: own LDS traffic complete, then s_barrier; VMEM stays in flight
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+#ifdef BCFFT_ABLATE
+// analysis build only (make ablate): phase switches set through bcfft_set_ablation(), and a
+// per-wave phase timeline (s_memtime at STAMP points) when bcfft_set_stamps() gave a buffer
+__device__ int g_ablate;
+__device__ unsigned long long* g_stamps;
+#define ABLATE(bit) (__builtin_amdgcn_readfirstlane(g_ablate) & (bit))
+#define STAMP_SLOTS 64
+#define STAMP(id)                                                                              \
+  do {                                                                                         \
+    unsigned long long* sp_ = g_stamps;                                                        \
+    if (sp_ && (threadIdx.x & 63) == 0) {                                                      \
+      unsigned long long t_;                                                                   \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_) :: "memory");           \
+      sp_[((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)) \
+          * STAMP_SLOTS + (id)] = t_;                                                          \
+    }                                                                                          \
+  } while (0)
+#else
+#define ABLATE(bit) 0
+#define STAMP(id) do {} while (0)
+#endif
 
 // ------------------------------------------------------------------ complex helpers
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
@@ -241,27 +284,37 @@ struct Fft {
     core<true>(row, gl, tw, v);
   }
 
-  // epilogue store of one transform's b outputs: y32 -> x dtype -> + bias -> y dtype
-  template <int XT>
+  // epilogue store of one transform's b outputs: y32 -> x dtype -> + bias -> y dtype.
+  // y dtype = promote(x dtype, bias dtype) is the x dtype or fp32 (YF32); bias is 16-B aligned.
+  template <int XT, bool YF32>
   static __device__ __forceinline__ void store(const float* row, int gl, void* yv, int64_t off,
-                                               const void* bias, int64_t bcol, int bias_dt, int y_dt) {
+                                               const void* bias, int64_t bcol, int bias_dt) {
 #pragma unroll
     for (int pc = 0; pc < B / (4 * L); ++pc) {
       const int p4 = (gl + L * pc) * 4;
       const float4 val = *reinterpret_cast<const float4*>(row + p4);
-      float vv[4] = {val.x, val.y, val.z, val.w};
+      float vv[4] = {round_to(val.x, XT), round_to(val.y, XT), round_to(val.z, XT),   // .to(x.dtype) :266
+                     round_to(val.w, XT)};
+      if (bias_dt != BCFFT_NONE) {                                                   // + bias :270-271
+        float bb[4];
+        if (bias_dt == BCFFT_F32) {
+          const float4 b4 = *reinterpret_cast<const float4*>((const float*)bias + bcol + p4);
+          bb[0] = b4.x; bb[1] = b4.y; bb[2] = b4.z; bb[3] = b4.w;
+        } else {
+          const uint2 b2 = *reinterpret_cast<const uint2*>((const uint16_t*)bias + bcol + p4);
+          const uint32_t w[4] = {b2.x & 0xffffu, b2.x >> 16, b2.y & 0xffffu, b2.y >> 16};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float r = round_to(vv[e], XT);                                         // .to(x.dtype) :266
-        if (bias_dt != BCFFT_NONE) r += load_scalar(bias, bcol + p4 + e, bias_dt);  // + bias :270-271
-        vv[e] = r;
+          for (int e = 0; e < 4; ++e) bb[e] = bias_dt == BCFFT_BF16 ? bf16_to_f32(w[e]) : f16_to_f32(w[e]);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) vv[e] += bb[e];
       }
-      if (y_dt == BCFFT_F32) {
+      if constexpr (YF32 || XT == BCFFT_F32) {
         *reinterpret_cast<float4*>((float*)yv + off + p4) = make_float4(vv[0], vv[1], vv[2], vv[3]);
       } else {
         uint32_t h[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) h[e] = y_dt == BCFFT_BF16 ? f32_to_bf16(vv[e]) : f32_to_f16(vv[e]);
+        for (int e = 0; e < 4; ++e) h[e] = XT == BCFFT_BF16 ? f32_to_bf16(vv[e]) : f32_to_f16(vv[e]);
         *reinterpret_cast<uint2*>((uint16_t*)yv + off + p4) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
       }
     }
@@ -356,11 +409,11 @@ struct GeoV {
   static_assert(BPL * OPL * TT * 2 == 128, "accumulator budget");
 };
 
-template <int B, int XT>
+template <int B, int XT, bool YF32>
 __global__ __launch_bounds__(512) void bc_forward_valu_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_in, int n_out,
     const float2* __restrict__ spec, const void* __restrict__ bias, int bias_dt,
-    void* __restrict__ yv, int y_dt) {
+    void* __restrict__ yv) {
   using G = GeoV<B>;
   using F = Fft<B>;
   constexpr int H = G::H, L = G::L, TT = G::TT, IC = G::IC, SROW = G::SROW, XROW = G::XROW;
@@ -519,7 +572,7 @@ __global__ __launch_bounds__(512) void bc_forward_valu_kernel(
       F::inverse(row, gl, tw, 0);
       const int64_t tok = t0 + t;
       if (tok < n_tokens && o < n_out)
-        F::template store<XT>(row, gl, yv, tok * M + (int64_t)o * B, bias, (int64_t)o * B, bias_dt, y_dt);
+        F::template store<XT, YF32>(row, gl, yv, tok * M + (int64_t)o * B, bias, (int64_t)o * B, bias_dt);
     }
   }
 }
@@ -532,21 +585,26 @@ __global__ __launch_bounds__(512) void bc_forward_valu_kernel(
 //   => D[(t,re)][o] = sum_i Re(C X), D[(t,im)][o] = sum_i Im(C X).
 //   Bin 0 (packed DC/Nyquist, both real): A = (X0, 0) / (0, X_H), B = (C0, C_H).
 //   Two MFMAs per tile: B = C_hi and B = C_lo -> (Xhi + Xlo)(Chi + Clo), fp32 accumulate.
+// x streams through two half-chunk LDS buffers by inline-asm LDS-DMA: half 0 of chunk c+1 is
+// issued as soon as the FFTs of half 0 of chunk c are done (it lands under the half-1 FFTs and
+// the MFMAs), half 1 after the MFMAs (it lands under the next half-0 FFTs). Waits are counted
+// (every wave issues exactly NH DMAs per half), barriers are raw s_barrier + lgkmcnt(0).
 template <int B>
 struct GeoM {
   using F = Fft<B>;
   static constexpr int H = B / 2, L = F::L, SROW = F::SROW;
   static constexpr int TT = 8, NW = 4, NT = NW * 64;   // 8 tokens = one MFMA row tile
-  static constexpr int KB = 8;                    // input blocks per chunk (MFMA K = 32)
+  static constexpr int KB = 8, KH = KB / 2;       // input blocks per chunk (MFMA K = 32) / half
   static constexpr int BPW = H / NW;              // bins per wave
   static constexpr int NTL = 32 / BPW;            // 16-output N-tiles per workgroup
   static constexpr int OUT_PER_WG = 16 * NTL;
   static constexpr int NGROUPS = NT / L;
-  static constexpr int ROWS = TT * KB;            // transforms per chunk
-  static constexpr int TPC = ROWS / NGROUPS;      // transforms per FFT group per chunk
+  static constexpr int HROWS = TT * KH;           // x rows per half-chunk, row r = (r / KH, r % KH)
+  static constexpr int HTPG = (HROWS + NGROUPS - 1) / NGROUPS;   // transforms per group per half
+  static constexpr int NH = HROWS / NW;           // DMA instructions per wave per half-chunk
   static constexpr int XS = 2 * TT * KB + 4;      // dwords per bin of the split-X image (+4 pad)
   static constexpr int MAIN_OFF = 2 * B;
-  static constexpr int STAGE_FLOATS = ROWS * SROW;
+  static constexpr int STAGE_FLOATS = 2 * HROWS * SROW;
   static constexpr int XL_OFF = MAIN_OFF + STAGE_FLOATS;
   static constexpr int XL_FLOATS = H * XS;
   static constexpr int EPI_ROWS = 16 * TT;        // one N-tile: 16 outputs x TT tokens
@@ -557,22 +615,25 @@ struct GeoM {
   static constexpr int RING = 4;                  // B-fragment prefetch depth (steps)
 
   static_assert(BPW * NTL * 4 == 128, "accumulator budget");
-  static_assert(ROWS % NGROUPS == 0 && EPI_ROWS % NGROUPS == 0, "group tiling");
+  static_assert(HROWS % NW == 0 && EPI_ROWS % NGROUPS == 0, "row tiling");
   static_assert(H >= 16, "bin swizzle needs H >= 16");
   static_assert(LDS_FLOATS * 4 <= 80 * 1024, "LDS budget: two workgroups per CU");
 };
 
-template <int B, int XT>
+template <int B, int XT, bool YF32>
 __global__ __launch_bounds__(256, 2) void bc_forward_mfma_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_in, int n_out,
     const float2* __restrict__ spec, const void* __restrict__ bias, int bias_dt,
-    void* __restrict__ yv, int y_dt, int dbg) {
+    void* __restrict__ yv) {
   using G = GeoM<B>;
   using F = Fft<B>;
-  constexpr int H = G::H, L = G::L, TT = G::TT, KB = G::KB, SROW = G::SROW, XS = G::XS;
-  constexpr int NTL = G::NTL, BPW = G::BPW, STEPS = G::STEPS, RING = G::RING;
+  constexpr int H = G::H, L = G::L, TT = G::TT, KB = G::KB, KH = G::KH, SROW = G::SROW, XS = G::XS;
+  constexpr int NTL = G::NTL, BPW = G::BPW, STEPS = G::STEPS, RING = G::RING, NH = G::NH;
+  constexpr int ES = XTraits<XT>::ES;
+  constexpr int DMA_LANES = B * ES / 16;          // one 16-B-per-lane DMA instruction per x row
+  static_assert(DMA_LANES <= 64, "x row fits one DMA instruction");
 
-    __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
+  __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
   float2* tw = reinterpret_cast<float2*>(lds);
   float* stage = lds + G::MAIN_OFF;
   uint32_t* xl = reinterpret_cast<uint32_t*>(lds + G::XL_OFF);
@@ -605,34 +666,40 @@ __global__ __launch_bounds__(256, 2) void bc_forward_mfma_kernel(
 #pragma unroll
     for (int nt = 0; nt < NTL; ++nt) acc[fb][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // x chunk -> LDS rows by LDS-DMA (raw dtype, row T = token*KB + block). One wave
-  // instruction moves 64 lanes x DS bytes of one row; rows stay padded to SROW floats.
-  auto dma_chunk = [&](int i0) {
-    constexpr int ES = XTraits<XT>::ES;
-    constexpr int ROW_BYTES = B * ES;
-    // LDS-DMA writes lane l's dword at base + 4l (also for sub-dword sizes), so rows shorter
-    // than 256 B use dword DMA with ROW_BYTES/4 active lanes
-    constexpr int IPR = ROW_BYTES >= 256 ? ROW_BYTES / 256 : 1;     // instructions per row
-    constexpr int ACTIVE = ROW_BYTES >= 256 ? 64 : ROW_BYTES / 4;    // lanes per instruction
-    constexpr int NINST = G::ROWS * IPR;
-    static_assert(NINST % G::NW == 0, "DMA instructions per wave");
+  // half-chunk h of the chunk starting at input block i0 -> stage buffer h, raw x dtype.
+  // Out-of-range rows read clamped (valid, finite-if-x-is) sources instead of branching, so every
+  // wave issues exactly NH DMAs: past-the-end tokens are never stored, and blocks >= n_in meet
+  // zero weights in the MFMA image.
+  const int64_t last_tok = n_tokens - 1;
+  auto dma_half = [&](int i0, int h) {
+#pragma unroll
+    for (int q = 0; q < NH; ++q) {
+      const int r = q * G::NW + wave;
+      const int t = r / KH, blk = h * KH + r % KH;
+      const int64_t tok = t0 + t < n_tokens ? t0 + t : last_tok;
+      const int ib = i0 + blk < n_in ? i0 + blk : 0;
+      const char* src = (const char*)xv + (tok * K + (int64_t)ib * B) * ES + lane * 16;
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(stage + (h * G::HROWS + r) * SROW));
+      if (ABLATE(16)) continue;
+      if (lane < DMA_LANES) dma16(src, dst);
+    }
+  };
+  // forward FFTs of half-chunk h -> split-X image [bin][prec][token][block]
+  auto fft_half = [&](int h) {
 #pragma unroll 1
-    for (int q0 = 0; q0 < NINST / G::NW; ++q0) {   // a real loop: keeps addresses out of VGPRs
-      const int q = q0 * G::NW + wave;
-      const int T = q / IPR, piece = q % IPR;
-      const int t = T / KB, blk = T % KB;
-      const int64_t tok = t0 + t;
-      char* dst = reinterpret_cast<char*>(stage + T * SROW) + piece * 256;
-      if (lane < ACTIVE) {
-        if (tok < n_tokens && i0 + blk < n_in) {
-          const char* src = (const char*)xv + (tok * K + (int64_t)(i0 + blk) * B) * ES + piece * 256 + lane * 4;
-          if (dbg & 32)     // debug: plain load + ds_write instead of LDS-DMA
-            reinterpret_cast<uint32_t*>(dst)[lane] = *reinterpret_cast<const uint32_t*>(src);
-          else
-          __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
-                                           (__attribute__((address_space(3))) void*)dst, 4, 0, 0);
-        } else {                                  // zero-fill rows past the end (no NaN garbage)
-          reinterpret_cast<uint32_t*>(dst)[lane] = 0u;
+    for (int u = 0; u < G::HTPG; ++u) {
+      const int r = g + G::NGROUPS * u;
+      if (r < G::HROWS) {                       // b <= 64: half the groups idle per half-chunk
+        float* rowp = stage + (h * G::HROWS + r) * SROW;
+        if (!ABLATE(4)) F::template forward<XT>(rowp, gl, tw);
+        uint32_t* dst = xl + (r / KH) * KB + h * KH + r % KH;
+#pragma unroll
+        for (int jj = 0; jj < F::P; ++jj) {
+          const int k = gl + L * jj;
+          uint32_t hi, lo;
+          split_bf16(F::untangle(rowp, k, tw), hi, lo);
+          dst[k * XS] = hi;
+          dst[k * XS + TT * KB] = lo;
         }
       }
     }
@@ -648,42 +715,31 @@ __global__ __launch_bounds__(256, 2) void bc_forward_mfma_kernel(
   };
 
   const int n_chunks = sl.n_chunk;
-  if (!(dbg & 16)) dma_chunk(0);
+  STAMP(0);
+  dma_half(0, 0);
+  dma_half(0, 1);
 
   for (int ch = 0; ch < n_chunks; ++ch) {
     const int i0 = ch * KB;
-    __syncthreads();   // x chunk landed (the barrier waits vmcnt(0)); MFMA phase done with xl
-    if ((dbg & 256) && ch == (dbg >> 16)) {   // debug: dump the staged x rows into y, stop
-      for (int i = tid; i < G::STAGE_FLOATS; i += G::NT) ((float*)yv)[t0 * M + i] = stage[i];
-      return;
-    }
+    const bool more = ch + 1 < n_chunks;
+    const int sb = 1 + 6 * (ch & 7);
+    STAMP(sb);
+    wait_vmcnt<NH>();     // half 0 of this chunk landed (half 1 may still be in flight) ...
+    lds_barrier();        // ... for every wave; the previous chunk's MFMAs are done with xl
+    STAMP(sb + 1);
+    fft_half(0);
+    STAMP(sb + 2);
+    wait_vmcnt<0>();      // half 1 landed (no other VMEM is outstanding here)
+    lds_barrier();        // every wave is done with stage half 0
+    STAMP(sb + 3);
+    if (more) dma_half(i0 + KB, 0);
     uint4 bring[RING][2];
 #pragma unroll
-    for (int s = 0; s < RING; ++s) load_b(ch, s, bring[s]);
-    __syncthreads();
-
-    // ---- forward FFTs: transform T = g + NGROUPS*u -> (token T / KB, block T % KB)
-#pragma unroll 1
-    for (int u = 0; u < G::TPC; ++u) {
-      const int T = g + G::NGROUPS * u;
-      float* rowp = stage + T * SROW;
-      if (!(dbg & 4)) F::template forward<XT>(rowp, gl, tw);
-      uint32_t* dst = xl + (T / KB) * KB + (T % KB);
-#pragma unroll
-      for (int jj = 0; jj < F::P; ++jj) {
-        const int k = gl + L * jj;
-        uint32_t hi, lo;
-        split_bf16(F::untangle(rowp, k, tw), hi, lo);
-        dst[k * XS] = hi;                    // [bin][prec][token][block]
-        dst[k * XS + TT * KB] = lo;
-      }
-    }
-    __syncthreads();
-    if ((dbg & 128) && ch == (dbg >> 16)) {   // debug: dump the split-X image into y, stop
-      for (int i = tid; i < G::XL_FLOATS; i += G::NT) ((uint32_t*)yv)[t0 * M + i] = xl[i];
-      return;
-    }
-    if (ch + 1 < n_chunks && !(dbg & 16)) dma_chunk(i0 + KB);    // next x chunk behind the MFMAs
+    for (int s = 0; s < RING; ++s) load_b(ch, s, bring[s]);   // behind the DMA: waits stay exact
+    fft_half(1);
+    STAMP(sb + 4);
+    lds_barrier();        // split-X image complete
+    STAMP(sb + 5);
 
     // ---- MFMA complex MAC over the chunk's 8 blocks
     uint4 afrag;
@@ -705,8 +761,8 @@ __global__ __launch_bounds__(256, 2) void bc_forward_mfma_kernel(
         afrag = raw;
       }
       uint4 bcur[2] = {bring[s % RING][0], bring[s % RING][1]};
-      if (s + RING < STEPS && !(dbg & 2)) load_b(ch, s + RING, bring[s % RING]);
-      if (dbg & 1) {   // ablation: keep the operands live, skip the MFMAs
+      if (s + RING < STEPS && !ABLATE(2)) load_b(ch, s + RING, bring[s % RING]);
+      if (ABLATE(1)) {   // keep the operands live, skip the MFMAs
         asm volatile("" :: "v"(bcur[0].x), "v"(bcur[1].x), "v"(afrag.x));
         continue;
       }
@@ -714,11 +770,13 @@ __global__ __launch_bounds__(256, 2) void bc_forward_mfma_kernel(
       acc[fb][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, bcur[0]), acc[fb][nt], 0, 0, 0);
       acc[fb][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, bcur[1]), acc[fb][nt], 0, 0, 0);
     }
+    if (more) dma_half(i0 + KB, 1);   // after the last B-fragment wait: lands under the next FFTs
   }
 
-  // ---- epilogue, one 16-output N-tile per round. D layout: col = lane & 15 (output),
-  //      row = 4*(lane >> 4) + r -> token 2*(lane >> 4) + (r >> 1), part r & 1.
-  //      LDS row R = o_local*TT + t holds bin f at complex column f ^ o_local (bank spread).
+  STAMP(49);
+  // ---- epilogue, one 16-output N-tile per round (no DMA is in flight any more). D layout:
+  //      col = lane & 15 (output), row = 4*(lane >> 4) + r -> token 2*(lane >> 4) + (r >> 1),
+  //      part r & 1. LDS row R = o_local*TT + t holds bin f at complex column f ^ o_local.
 #pragma unroll
   for (int nt = 0; nt < NTL; ++nt) {
     __syncthreads();
@@ -732,17 +790,19 @@ __global__ __launch_bounds__(256, 2) void bc_forward_mfma_kernel(
       *reinterpret_cast<float2*>(p + SROW) = make_float2(a[2], a[3]);
     }
     __syncthreads();
+    STAMP(50 + 2 * nt);
 #pragma unroll 1
     for (int u2 = 0; u2 < G::EPI_ROWS / G::NGROUPS; ++u2) {
       const int R = g + G::NGROUPS * u2;
       const int ol = R / TT, t = R % TT;
       const int o = o_base + 16 * nt + ol;
       float* rowp = stage + R * SROW;
-      if (!(dbg & 8)) F::inverse(rowp, gl, tw, ol);
+      if (!ABLATE(8)) F::inverse(rowp, gl, tw, ol);
       const int64_t tok = t0 + t;
       if (tok < n_tokens && o < n_out)
-        F::template store<XT>(rowp, gl, yv, tok * M + (int64_t)o * B, bias, (int64_t)o * B, bias_dt, y_dt);
+        F::template store<XT, YF32>(rowp, gl, yv, tok * M + (int64_t)o * B, bias, (int64_t)o * B, bias_dt);
     }
+    STAMP(51 + 2 * nt);
   }
 }
 
@@ -846,41 +906,34 @@ bool valid_dt(int d) { return d == BCFFT_F32 || d == BCFFT_F16 || d == BCFFT_BF1
 bool valid_block(int b) { return b == 32 || b == 64 || b == 128 || b == 256; }
 int promote(int a, int b) { return (b == BCFFT_NONE || a == b) ? a : BCFFT_F32; }
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
-// Analysis switches (BCFFT_DEBUG_FLAGS; results are WRONG when set; production never sets it):
-// ablation: 1 skip MFMAs, 2 skip B-fragment loads, 4 skip forward FFT math, 8 skip inverse FFT
-// math, 16 skip x prefetch loads, 32 plain loads instead of LDS-DMA, 64 force one workgroup
-// per CU; LDS dumps (chunk = flags >> 16, written into the tile's y rows, then return):
-// 128 split-X image after the FFT phase, 256 staged x rows after the load (tools/dump_check.py).
-int debug_flags() {
-  const char* e = getenv("BCFFT_DEBUG_FLAGS");
-  return e ? atoi(e) : 0;
-}
-
-template <int B, int XT>
+template <int B, int XT, bool YF32>
 void launch_forward(int algo, const void* x, int64_t n, int n_in, int n_out, const void* spec,
-                    const void* bias, int bias_dt, void* y, int y_dt, hipStream_t s) {
+                    const void* bias, int bias_dt, void* y, hipStream_t s) {
   if constexpr (B <= 128) {
     if (algo == BCFFT_ALGO_MFMA) {
       using G = bcfft::GeoM<B>;
       dim3 grid((unsigned)((n + G::TT - 1) / G::TT), (unsigned)((n_out + G::OUT_PER_WG - 1) / G::OUT_PER_WG));
-      const int dbg = debug_flags();   // 64: pad dynamic LDS to force one workgroup per CU
-      hipLaunchKernelGGL((bcfft::bc_forward_mfma_kernel<B, XT>), grid, dim3(G::NT), (dbg & 64) ? 65536 : 0, s, x, n,
-                         n_in, n_out, (const float2*)spec, bias, bias_dt, y, y_dt, dbg);
+      hipLaunchKernelGGL((bcfft::bc_forward_mfma_kernel<B, XT, YF32>), grid, dim3(G::NT), 0, s, x, n,
+                         n_in, n_out, (const float2*)spec, bias, bias_dt, y);
       return;
     }
   }
   using G = bcfft::GeoV<B>;
   dim3 grid((unsigned)((n + G::TT - 1) / G::TT), (unsigned)((n_out + G::OUT_PER_WG - 1) / G::OUT_PER_WG));
-  hipLaunchKernelGGL((bcfft::bc_forward_valu_kernel<B, XT>), grid, dim3(G::NT), 0, s, x, n, n_in,
-                     n_out, (const float2*)spec, bias, bias_dt, y, y_dt);
+  hipLaunchKernelGGL((bcfft::bc_forward_valu_kernel<B, XT, YF32>), grid, dim3(G::NT), 0, s, x, n, n_in,
+                     n_out, (const float2*)spec, bias, bias_dt, y);
 }
 
 template <int B>
 void launch_forward_b(int algo, int xdt, const void* x, int64_t n, int n_in, int n_out,
                       const void* spec, const void* bias, int bias_dt, void* y, int y_dt, hipStream_t s) {
-  if (xdt == BCFFT_F32) launch_forward<B, BCFFT_F32>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, y_dt, s);
-  else if (xdt == BCFFT_F16) launch_forward<B, BCFFT_F16>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, y_dt, s);
-  else launch_forward<B, BCFFT_BF16>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, y_dt, s);
+  // y dtype = promote(x dtype, bias dtype): the x dtype, or fp32 for 16-bit x with another bias dtype
+  const bool yf32 = y_dt == BCFFT_F32;
+  if (xdt == BCFFT_F32) launch_forward<B, BCFFT_F32, true>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, s);
+  else if (xdt == BCFFT_F16 && yf32) launch_forward<B, BCFFT_F16, true>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, s);
+  else if (xdt == BCFFT_F16) launch_forward<B, BCFFT_F16, false>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, s);
+  else if (yf32) launch_forward<B, BCFFT_BF16, true>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, s);
+  else launch_forward<B, BCFFT_BF16, false>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, s);
 }
 
 template <int B>
@@ -908,7 +961,7 @@ const char* bcfft_status_string(int status) {
     case BCFFT_ERR_SHAPE: return "shape error: features must be positive multiples of block_size";
     case BCFFT_ERR_BLOCK: return "unsupported block_size (supported: 32, 64, 128, 256)";
     case BCFFT_ERR_DTYPE: return "unsupported dtype or y dtype != promote(x dtype, bias dtype)";
-    case BCFFT_ERR_ALIGN: return "x, y and spectra must be 16-byte aligned";
+    case BCFFT_ERR_ALIGN: return "x, y, spectra and bias must be 16-byte aligned";
     case BCFFT_ERR_HIP: return "HIP launch failed";
     case BCFFT_ERR_ARG: return "NULL pointer or invalid argument";
     default: return "unknown status";
@@ -955,7 +1008,7 @@ int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_feat
   if (algo != BCFFT_ALGO_AUTO && algo != BCFFT_ALGO_MFMA && algo != BCFFT_ALGO_VALU) return BCFFT_ERR_ARG;
   if (n_tokens == 0) return BCFFT_OK;
   if (!x || !y || !spectra) return BCFFT_ERR_ARG;
-  if (!aligned16(x) || !aligned16(y) || !aligned16(spectra)) return BCFFT_ERR_ALIGN;
+  if (!aligned16(x) || !aligned16(y) || !aligned16(spectra) || (bias && !aligned16(bias))) return BCFFT_ERR_ALIGN;
   const int n_in = in_features / block_size, n_out = out_features / block_size;
   if (algo == BCFFT_ALGO_AUTO) algo = block_size <= 128 ? BCFFT_ALGO_MFMA : BCFFT_ALGO_VALU;
   hipStream_t s = (hipStream_t)stream;
@@ -974,6 +1027,21 @@ int bcfft_forward(const void* x, int x_dtype, int64_t n_tokens, int in_features,
   return bcfft_forward_algo(x, x_dtype, n_tokens, in_features, out_features, block_size, spectra,
                             bias, bias_dtype, y, y_dtype, BCFFT_ALGO_AUTO, stream);
 }
+
+#ifdef BCFFT_ABLATE
+// analysis build only: phase switches of the MFMA kernel (results are WRONG when set):
+// 1 skip MFMAs, 2 skip B-fragment loads, 4 skip forward FFT math, 8 skip inverse FFT math,
+// 16 skip x DMA
+int bcfft_set_ablation(int flags) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(bcfft::g_ablate), &flags, sizeof(int)) == hipSuccess ? BCFFT_OK : BCFFT_ERR_HIP;
+}
+// phase timeline: 64 u64 slots per wave (s_memtime), indexed (block * waves + wave) * 64 + id;
+// NULL switches stamping off
+int bcfft_set_stamps(void* buf) {
+  unsigned long long* p = (unsigned long long*)buf;
+  return hipMemcpyToSymbol(HIP_SYMBOL(bcfft::g_stamps), &p, sizeof(p)) == hipSuccess ? BCFFT_OK : BCFFT_ERR_HIP;
+}
+#endif
 
 int bcfft_circulant_matvec(const void* c, const void* x, int dtype, int n, void* y, void* stream) {
   if (!c || !x || !y) return BCFFT_ERR_ARG;

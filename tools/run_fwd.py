@@ -1,5 +1,5 @@
 """Run the BC forward a few times (for rocprofv3 counter passes / traces).
-usage: run_fwd.py K M B IO N ITERS   (env BCFFT_ALGO / BCFFT_DEBUG_FLAGS honoured)"""
+usage: run_fwd.py K M B IO N ITERS   (env BCFFT_ALGO honoured)"""
 import os
 import sys
 
