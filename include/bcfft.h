@@ -30,12 +30,19 @@ extern "C" {
 
 enum bcfft_dtype { BCFFT_NONE = -1, BCFFT_F32 = 0, BCFFT_F16 = 1, BCFFT_BF16 = 2 };
 
-/* Forward algorithms (bcfft_forward_algo). Both are single fused launches.
+/* Forward algorithms (bcfft_forward_algo). All are single fused launches.
+ *  STAT: stationary weights. One persistent workgroup per CU keeps its output group's weight
+ *        spectra in VGPRs as fp16 MFMA fragments (scaled by a power of two) for the whole
+ *        launch, and streams tokens in tiles of 4. X is split into fp16 hi + lo under a
+ *        per-token power-of-two scale, with fp32 accumulation: ~3e-4 relative (the fp16
+ *        rounding of the weight spectra), inside the 1e-3 contract.
+ *        Geometries: block_size 128 with in_features 4096, block_size 64 with in_features
+ *        2048 or 4096; any out_features. BCFFT_ERR_BLOCK for others.
  *  MFMA: per-bin complex MAC on the matrix cores as a bf16 GEMM with hi/lo splitting of both
  *        operands ((Xhi+Xlo)(Chi+Clo), fp32 accumulate; ~1e-5 relative). block_size <= 128.
  *  VALU: per-bin complex MAC in fp32 FMAs (the reference's fp32 arithmetic). Any block size.
- *  AUTO: MFMA for block_size <= 128, VALU otherwise. */
-enum bcfft_algo { BCFFT_ALGO_AUTO = 0, BCFFT_ALGO_MFMA = 1, BCFFT_ALGO_VALU = 2 };
+ *  AUTO: STAT where eligible, else MFMA for block_size <= 128, else VALU. */
+enum bcfft_algo { BCFFT_ALGO_AUTO = 0, BCFFT_ALGO_MFMA = 1, BCFFT_ALGO_VALU = 2, BCFFT_ALGO_STAT = 3 };
 
 enum bcfft_status {
   BCFFT_OK = 0,
@@ -57,8 +64,9 @@ const char* bcfft_status_string(int status);
 const char* bcfft_last_hip_error(void);
 
 /* Bytes of the spectra buffer of an operator with (n_out_blocks x n_in_blocks) b x b
- * circulant blocks: packed fp32 bins (n_out*n_in*b/2 complex64), a b-entry twiddle table
- * and, for b <= 128, the split-bf16 image the MFMA kernel streams. */
+ * circulant blocks: packed fp32 bins (n_out*n_in*b/2 complex64), a b-entry twiddle table,
+ * for b <= 128 the split-bf16 image the MFMA kernel streams and, for STAT geometries, the
+ * scaled fp16 fragment image the STAT kernel keeps in registers. */
 int64_t bcfft_spectra_bytes(int n_out_blocks, int n_in_blocks, int block_size);
 
 /* Packed weight spectra. Replaces `Cf = torch.fft.rfft(self.c.to(float32), dim=-1)`

@@ -41,7 +41,7 @@ def spectra(c: torch.Tensor, transpose_conj: bool = False) -> torch.Tensor:
 
 
 def default_algo() -> str:
-    """BCFFT_ALGO env var: auto (default) | mfma | valu."""
+    """BCFFT_ALGO env var: auto (default) | stationary | mfma | valu."""
     import os
     a = os.environ.get("BCFFT_ALGO", "auto").lower()
     if a not in _lib.ALGOS:
@@ -52,7 +52,9 @@ def default_algo() -> str:
 def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, block_size: int,
             out_features: int, algo: str | None = None) -> torch.Tensor:
     """y = BC(x2d) (+ bias) with one fused kernel. x2d: (N, K) device tensor.
-    algo: "auto" (MFMA for b <= 128), "mfma" or "valu" (exact fp32 MAC)."""
+    algo: "auto" (stationary where eligible, else mfma for b <= 128, else valu),
+    "stationary" (weights in VGPRs, fp16 MFMA, ~3e-4), "mfma" (split-bf16, ~1e-5) or
+    "valu" (exact fp32 MAC). See include/bcfft.h."""
     _lib.require_device(x2d, "bcfft.forward")
     n, k = x2d.shape
     x2d = x2d.contiguous()

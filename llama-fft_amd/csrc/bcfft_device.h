@@ -1,0 +1,399 @@
+// bcfft_device.h — device helpers shared by the gfx950 kernels of libbcfft.so (internal).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bcfft.h"
+
+namespace bcfft {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+// ------------------------------------------------------------------ scalar conversions
+__device__ __forceinline__ float bf16_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
+__device__ __forceinline__ uint32_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;  // keep NaN a (quiet) NaN
+  u += 0x7fffu + ((u >> 16) & 1u);                                 // round to nearest even
+  return u >> 16;
+}
+__device__ __forceinline__ float f16_to_f32(uint32_t h) {
+  _Float16 v;
+  uint16_t s = (uint16_t)h;
+  __builtin_memcpy(&v, &s, 2);
+  return (float)v;
+}
+__device__ __forceinline__ uint32_t f32_to_f16(float f) {
+  _Float16 v = (_Float16)f;
+  uint16_t s;
+  __builtin_memcpy(&s, &v, 2);
+  return s;
+}
+// value-exact emulation of tensor.to(dtype) read back as fp32
+__device__ __forceinline__ float round_to(float v, int dt) {
+  if (dt == BCFFT_BF16) return bf16_to_f32(f32_to_bf16(v));
+  if (dt == BCFFT_F16) return f16_to_f32(f32_to_f16(v));
+  return v;
+}
+__device__ __forceinline__ float load_scalar(const void* p, int64_t i, int dt) {
+  if (dt == BCFFT_F32) return ((const float*)p)[i];
+  uint32_t h = ((const uint16_t*)p)[i];
+  return dt == BCFFT_BF16 ? bf16_to_f32(h) : f16_to_f32(h);
+}
+// v = hi + lo with hi, lo bf16: returns packed (lo16 = first, hi16 = second) pairs. Internal
+// MFMA operands only, so the hardware RNE conversion (v_cvt_pk_bf16_f32, one instruction per
+// pair) is used; outputs keep the bit-exact software rounding above.
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+__device__ __forceinline__ void split_bf16(float2 v, uint32_t& hi, uint32_t& lo) {
+  const bf16x2 h = {(__bf16)v.x, (__bf16)v.y};
+  hi = __builtin_bit_cast(uint32_t, h);
+  const bf16x2 l = {(__bf16)(v.x - __uint_as_float(hi << 16)),
+                    (__bf16)(v.y - __uint_as_float(hi & 0xffff0000u))};
+  lo = __builtin_bit_cast(uint32_t, l);
+}
+
+// ------------------------------------------------------------------ LDS-DMA (inline asm)
+// hipcc neither counts an asm load in its s_waitcnt bookkeeping nor drains it at a barrier, so
+// the x stream stays in flight across compute phases; every wait on it is explicit below.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+// LDS[m0 + 16 * lane] <- 16 B at the lane's global address (m0 = wave-uniform LDS byte address)
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  // a real S_WAITCNT (not inline asm): the compiler's waitcnt pass sees it and knows every older
+  // load has landed, so it adds no vmcnt(0) of its own later (those drain in-flight DMA/stores)
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+  asm volatile("" ::: "memory");
+}
+// workgroup rendezvous on LDS: own LDS traffic complete, then s_barrier; VMEM stays in flight
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+#ifdef BCFFT_ABLATE
+// analysis build only (make ablate): phase switches set through bcfft_set_ablation(), and a
+// per-wave phase timeline (s_memtime at STAMP points) when bcfft_set_stamps() gave a buffer
+// (static: each translation unit has its own copy and its own setter). ANALYSIS_INIT reads both
+// ONCE per kernel into scalars: a per-use read would be a global load + s_waitcnt vmcnt(0) that
+// drains every in-flight store and DMA, i.e. the measurement would serialise the kernel.
+static __device__ int g_ablate;
+static __device__ unsigned long long* g_stamps;
+#define ANALYSIS_INIT                                                                          \
+  const int ablate_flags_ = __builtin_amdgcn_readfirstlane(g_ablate);                          \
+  unsigned long long* const stamps_ = g_stamps;                                                \
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory")
+#define ABLATE(bit) (ablate_flags_ & (bit))
+#define STAMP_SLOTS 64
+#define STAMP(id)                                                                              \
+  do {                                                                                         \
+    if (stamps_ && (threadIdx.x & 63) == 0) {                                                  \
+      unsigned long long t_;                                                                   \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_) :: "memory");           \
+      stamps_[((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)) \
+          * STAMP_SLOTS + (id)] = t_;                                                          \
+    }                                                                                          \
+  } while (0)
+#else
+#define ANALYSIS_INIT do {} while (0)
+#define ABLATE(bit) 0
+#define STAMP(id) do {} while (0)
+#endif
+
+// ------------------------------------------------------------------ complex helpers
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 w) {
+  return make_float2(fmaf(a.x, w.x, -a.y * w.y), fmaf(a.x, w.y, a.y * w.x));
+}
+__device__ __forceinline__ float2 cmulc(float2 a, float2 w) {  // a * conj(w)
+  return make_float2(fmaf(a.x, w.x, a.y * w.y), fmaf(a.y, w.x, -a.x * w.y));
+}
+
+// exp(-2*pi*i*m/16) for m < 8: the constant twiddles of the in-register radix-2 DFTs
+__device__ __forceinline__ float2 tw16(int m) {
+  constexpr float C1 = 0.92387953251128674f, S1 = 0.38268343236508978f, R = 0.70710678118654752f;
+  switch (m) {
+    case 1: return make_float2(C1, -S1);
+    case 2: return make_float2(R, -R);
+    case 3: return make_float2(S1, -C1);
+    case 5: return make_float2(-S1, -C1);
+    case 6: return make_float2(-R, -R);
+    case 7: return make_float2(-C1, -S1);
+    default: return make_float2(1.f, 0.f);
+  }
+}
+
+template <bool INV>
+__device__ __forceinline__ float2 twiddle16(float2 b, int m) {  // b * W16^m (conj if INV)
+  if (m == 0) return b;
+  if (m == 4) return INV ? make_float2(-b.y, b.x) : make_float2(b.y, -b.x);
+  float2 w = tw16(m);
+  return INV ? cmulc(b, w) : cmul(b, w);
+}
+
+template <int N>
+constexpr int bitrev(int x) {
+  int r = 0;
+  for (int i = 1; i < N; i <<= 1) { r = (r << 1) | (x & 1); x >>= 1; }
+  return r;
+}
+
+// In-register N-point DFT (N = 2,4,8,16), natural order in and out.
+// Forward: sum_n v[n] e^{-2 pi i nk/N}; INV: e^{+2 pi i nk/N} (unnormalised).
+template <int N, bool INV>
+__device__ __forceinline__ void dft(float2 (&v)[N]) {
+  float2 t[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) t[i] = v[bitrev<N>(i)];
+#pragma unroll
+  for (int len = 2; len <= N; len <<= 1) {
+#pragma unroll
+    for (int s = 0; s < N; s += len) {
+#pragma unroll
+      for (int j = 0; j < len / 2; ++j) {
+        float2 a = t[s + j];
+        float2 b = twiddle16<INV>(t[s + j + len / 2], j * (16 / len));
+        t[s + j] = cadd(a, b);
+        t[s + j + len / 2] = csub(a, b);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = t[i];
+}
+
+// LDS ordering between lanes of ONE wave (the lanes of an FFT group share a wave):
+// DS instructions of a wave execute in order; this only stops the compiler from moving
+// LDS accesses across the point.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ------------------------------------------------------------------ FFT building blocks
+// One transform per L-lane group, on an LDS row of SROW floats.
+template <int B>
+struct Fft {
+  static constexpr int H = B / 2;                 // complex FFT length / packed bins
+  static constexpr int L = (H <= 32) ? 4 : 8;     // lanes per transform (four-step H = L x P)
+  static constexpr int P = H / L;                 // points per lane
+  static constexpr int Q = P / L > 0 ? P / L : 1; // k2 values per lane in step 2
+  static constexpr int ROWA = B + 2 * L;
+  static constexpr int ROWB = 2 * P * (L + 1);
+  static constexpr int SROW = ((ROWA > ROWB ? ROWA : ROWB) + 3) / 4 * 4;
+
+  // steps 1-2 of the four-step FFT on v (v[n2] = z[gl + L*n2]); on return the row holds
+  // the result in natural order (complex index k at floats 2k, 2k+1).
+  template <bool INV>
+  static __device__ __forceinline__ void core(float* row, int gl, const float2* tw, float2 (&v)[P]) {
+    dft<P, INV>(v);
+#pragma unroll
+    for (int k2 = 1; k2 < P; ++k2) {                                  // W_H^(+-n1 k2)
+      const float2 w = tw[(2 * gl * k2) % B];
+      v[k2] = INV ? cmulc(v[k2], w) : cmul(v[k2], w);
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int k2 = 0; k2 < P; ++k2)                                    // transpose through the row
+      *reinterpret_cast<float2*>(row + 2 * (k2 * (L + 1) + gl)) = v[k2];
+    wave_lds_sync();
+    float2 u[Q][L];
+#pragma unroll
+    for (int m = 0; m < Q; ++m)
+#pragma unroll
+      for (int n1 = 0; n1 < L; ++n1)
+        u[m][n1] = *reinterpret_cast<const float2*>(row + 2 * ((gl + L * m) * (L + 1) + n1));
+#pragma unroll
+    for (int m = 0; m < Q; ++m) dft<L, INV>(u[m]);
+    wave_lds_sync();
+#pragma unroll
+    for (int m = 0; m < Q; ++m)
+#pragma unroll
+      for (int k1 = 0; k1 < L; ++k1)                                  // index P*k1 + k2
+        *reinterpret_cast<float2*>(row + 2 * (P * k1 + gl + L * m)) = u[m][k1];
+    wave_lds_sync();
+  }
+
+  // forward: row holds x (B reals, fp32 or the raw 16-bit input when RAW16 is the dtype);
+  // afterwards Z = FFT_H(x_even + i x_odd) in natural order (fp32 complex)
+  template <int RAW = BCFFT_F32>
+  static __device__ __forceinline__ void forward(float* row, int gl, const float2* tw) {
+    float2 v[P];
+#pragma unroll
+    for (int n2 = 0; n2 < P; ++n2) {
+      const int j = gl + L * n2;
+      if constexpr (RAW == BCFFT_F32) {
+        v[n2] = *reinterpret_cast<const float2*>(row + 2 * j);
+      } else {
+        const uint32_t w = reinterpret_cast<const uint32_t*>(row)[j];
+        v[n2] = RAW == BCFFT_BF16 ? make_float2(bf16_to_f32(w & 0xffffu), bf16_to_f32(w >> 16))
+                                  : make_float2(f16_to_f32(w & 0xffffu), f16_to_f32(w >> 16));
+      }
+    }
+    core<false>(row, gl, tw, v);
+  }
+
+  // packed spectrum X'[k] = 2 X[k] (bin 0: (2 X_0, 2 X_{H})) from Z in the row
+  static __device__ __forceinline__ float2 untangle(const float* row, int k, const float2* tw) {
+    const float2 zk = *reinterpret_cast<const float2*>(row + 2 * k);
+    const float2 zh = *reinterpret_cast<const float2*>(row + 2 * ((H - k) & (H - 1)));
+    const float sr = zk.x + zh.x, si = zk.y - zh.y;   // Zk + conj(Z[H-k])
+    const float dr = zk.x - zh.x, di = zk.y + zh.y;   // Zk - conj(Z[H-k])
+    const float2 w = tw[k];
+    float2 o;
+    o.x = sr + w.x * di + w.y * dr;                    // (Zk+Zm) - i W^k (Zk-Zm)
+    o.y = si - w.x * dr + w.y * di;
+    if (k == 0) o = make_float2(2.f * (zk.x + zk.y), 2.f * (zk.x - zk.y));
+    return o;
+  }
+
+  // inverse: the row holds packed Y (complex index k stored at column k ^ swz); afterwards
+  // it holds the b real outputs y[0..B) in order (1/b already folded into the spectra).
+  static __device__ __forceinline__ void inverse(float* row, int gl, const float2* tw, int swz) {
+    float2 v[P];
+#pragma unroll
+    for (int n2 = 0; n2 < P; ++n2) {
+      const int k = gl + L * n2;
+      const float2 yk = *reinterpret_cast<const float2*>(row + 2 * (k ^ swz));
+      const float2 yh = *reinterpret_cast<const float2*>(row + 2 * (((H - k) & (H - 1)) ^ swz));
+      const float er = yk.x + yh.x, ei = yk.y - yh.y;   // E = Y[k] + conj(Y[H-k])
+      const float dr = yk.x - yh.x, di = yk.y + yh.y;   // D = Y[k] - conj(Y[H-k])
+      const float2 w = tw[k];                           // O = D conj(W^k); Zi = E + iO
+      float2 z;
+      z.x = er - (di * w.x - dr * w.y);
+      z.y = ei + (dr * w.x + di * w.y);
+      if (k == 0) z = make_float2(yk.x + yk.y, yk.x - yk.y);   // packed bin 0
+      v[n2] = z;
+    }
+    core<true>(row, gl, tw, v);
+  }
+
+  // epilogue store of one transform's b outputs: y32 -> x dtype -> + bias -> y dtype.
+  // y dtype = promote(x dtype, bias dtype) is the x dtype or fp32 (YF32); bias is 16-B aligned.
+  template <int XT, bool YF32>
+  static __device__ __forceinline__ void store(const float* row, int gl, void* yv, int64_t off,
+                                               const void* bias, int64_t bcol, int bias_dt) {
+#pragma unroll
+    for (int pc = 0; pc < B / (4 * L); ++pc) {
+      const int p4 = (gl + L * pc) * 4;
+      const float4 val = *reinterpret_cast<const float4*>(row + p4);
+      float vv[4] = {round_to(val.x, XT), round_to(val.y, XT), round_to(val.z, XT),   // .to(x.dtype) :266
+                     round_to(val.w, XT)};
+      if (bias_dt != BCFFT_NONE) {                                                   // + bias :270-271
+        float bb[4];
+        if (bias_dt == BCFFT_F32) {
+          const float4 b4 = *reinterpret_cast<const float4*>((const float*)bias + bcol + p4);
+          bb[0] = b4.x; bb[1] = b4.y; bb[2] = b4.z; bb[3] = b4.w;
+        } else {
+          const uint2 b2 = *reinterpret_cast<const uint2*>((const uint16_t*)bias + bcol + p4);
+          const uint32_t w[4] = {b2.x & 0xffffu, b2.x >> 16, b2.y & 0xffffu, b2.y >> 16};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bb[e] = bias_dt == BCFFT_BF16 ? bf16_to_f32(w[e]) : f16_to_f32(w[e]);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) vv[e] += bb[e];
+      }
+      if constexpr (YF32 || XT == BCFFT_F32) {
+        *reinterpret_cast<float4*>((float*)yv + off + p4) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+      } else {
+        uint32_t h[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) h[e] = XT == BCFFT_BF16 ? f32_to_bf16(vv[e]) : f32_to_f16(vv[e]);
+        *reinterpret_cast<uint2*>((uint16_t*)yv + off + p4) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+      }
+    }
+  }
+};
+
+template <int XT> struct XTraits;
+template <> struct XTraits<BCFFT_F32> { static constexpr int ES = 4; };
+template <> struct XTraits<BCFFT_F16> { static constexpr int ES = 2; };
+template <> struct XTraits<BCFFT_BF16> { static constexpr int ES = 2; };
+
+// 16 B of x (VEC elements) -> fp32 in LDS
+template <int XT>
+__device__ __forceinline__ void stage_store(float* dst, uint4 v) {
+  if constexpr (XT == BCFFT_F32) {
+    *reinterpret_cast<uint4*>(dst) = v;
+  } else {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    float f[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if constexpr (XT == BCFFT_BF16) {
+        f[2 * k] = bf16_to_f32(w[k] & 0xffffu);
+        f[2 * k + 1] = bf16_to_f32(w[k] >> 16);
+      } else {
+        f[2 * k] = f16_to_f32(w[k] & 0xffffu);
+        f[2 * k + 1] = f16_to_f32(w[k] >> 16);
+      }
+    }
+    *reinterpret_cast<float4*>(dst) = make_float4(f[0], f[1], f[2], f[3]);
+    *reinterpret_cast<float4*>(dst + 4) = make_float4(f[4], f[5], f[6], f[7]);
+  }
+}
+
+// ------------------------------------------------------------------ spectra buffer layout
+// [packed fp32: nO*nI*H float2][twiddles: B float2][MFMA image (b <= 128)][stationary image]
+// MFMA image: dword ((c*H + f)*2 + prec)*nOp*8 + o*8 + j  = split-bf16 pair of bin f of
+// block (o, 8c + j): bin 0 (C0, C_H) as is, other bins conj(C); prec 0 = hi, 1 = lo.
+// Stationary image (stat_eligible geometries, bc_forward_stat_kernel): 16-B header
+// {s_C, 1/s_C, 0, 0} then, per output group of 32 blocks, per wave (8), per register piece,
+// per lane, the 16-B fp16 B fragment that lane keeps in VGPRs for the whole launch
+// (bcfft_stat.hip has the exact map).
+struct SpecLayout {
+  int64_t packed_f2, tw_off_f2, img_off_u32, img_u32, stat_off_u32, stat_u32, total_bytes;
+  int n_chunk, n_out_pad, stat_groups, stat_pieces;
+};
+__host__ __device__ inline int mfma_out_per_wg(int b) { return 4096 / b; }   // 16 * NTL
+// stationary-weight kernel geometries: fp16 B fragments of 32 output blocks x all inputs fit
+// 128 VGPRs per lane of 8 waves (K <= 4096), and the A image swizzle needs >= 8 block quads
+__host__ __device__ inline bool stat_eligible(int n_in, int b) {
+  return (b == 128 && n_in == 32) || (b == 64 && (n_in == 32 || n_in == 64));
+}
+constexpr int STAT_OUT_BLOCKS = 32;    // output blocks per stationary group (two 16-wide N-tiles)
+__host__ __device__ inline SpecLayout spec_layout(int n_out, int n_in, int b) {
+  SpecLayout s;
+  const int h = b / 2;
+  s.packed_f2 = (int64_t)n_out * n_in * h;
+  s.tw_off_f2 = s.packed_f2;
+  const int64_t head_f2 = s.packed_f2 + b;
+  s.img_off_u32 = head_f2 * 2;
+  if (b <= 128) {
+    const int opw = mfma_out_per_wg(b);
+    s.n_chunk = (n_in + 7) / 8;
+    s.n_out_pad = (n_out + opw - 1) / opw * opw;
+    s.img_u32 = (int64_t)s.n_chunk * h * 2 * s.n_out_pad * 8;
+  } else {
+    s.n_chunk = 0;
+    s.n_out_pad = 0;
+    s.img_u32 = 0;
+  }
+  s.stat_off_u32 = s.img_off_u32 + s.img_u32;
+  if (stat_eligible(n_in, b)) {
+    s.stat_groups = (n_out + STAT_OUT_BLOCKS - 1) / STAT_OUT_BLOCKS;
+    s.stat_pieces = (h / 8) * (n_in / 16) * 2;          // bins/wave x K-steps x N-tiles
+    s.stat_u32 = 4 + (int64_t)s.stat_groups * 8 * s.stat_pieces * 64 * 4;
+  } else {
+    s.stat_groups = 0;
+    s.stat_pieces = 0;
+    s.stat_u32 = 0;
+  }
+  s.total_bytes = (s.stat_off_u32 + s.stat_u32) * 4;
+  return s;
+}
+
+// host launchers of the stationary-weight kernel (bcfft_stat.hip); return false when the
+// geometry / dtype combination has no instantiation
+bool launch_forward_stat(int b, int n_in, int xdt, bool yf32, const void* x, int64_t n, int n_out,
+                         const void* spec, const void* bias, int bias_dt, void* y, hipStream_t s);
+void launch_stat_image(int b, int n_out, int n_in, void* spec, hipStream_t s);
+
+}  // namespace bcfft

@@ -1,0 +1,759 @@
+// bcfft_stat.hip — stationary-weight block-circulant forward for gfx950 (MI355X).
+//
+// Same operator as bc_forward_mfma_kernel (BlockCirculantLinear.forward,
+// patch_llama_fft.py:226-275), organised the other way round: the WEIGHTS stay in registers
+// and the TOKENS stream.
+//
+//  * One persistent 512-thread workgroup per CU (8 waves, 2 per SIMD, <= 256 VGPRs). Each
+//    workgroup owns one output group of 32 blocks (= 4096 outputs at b = 128). It loads that
+//    group's packed weight spectra ONCE, as fp16 MFMA B fragments scaled by a power of two
+//    s_C: K/32 = 128 VGPRs per lane. Wave w keeps bins [w*BW, (w+1)*BW).
+//  * Tokens go through in M-tiles of 4. x arrives by LDS-DMA into one of two 64 KiB regions,
+//    one M-tile ahead. Each M-tile runs three phases, separated by workgroup barriers:
+//      forward  one row (token, input block) per L = b/32 lanes, 16 complex points per lane:
+//               an in-register 16-point DFT, the four-step twiddle, an L-point DFT across the
+//               lanes (DPP), then the real-FFT untangle (partner bin from DPP). The result is
+//               scaled by a per-token power of two s_t, split into fp16 hi + lo, and written as
+//               the MFMA A image in place over x.
+//      CMAC     per bin: v_mfma_f32_16x16x32_f16 with rows (token, re/im, hi/lo) x 16 output
+//               blocks, K = 16 input blocks x (re, im); B = stationary conj(C) fragments.
+//               The per-bin results go to LDS rows (token, output block).
+//      inverse  the real-FFT pre-process from LDS, a 16-point DFT, twiddle, L-point DFT across
+//               the lanes, scale 1/(s_t s_C), cast/bias/cast, then 16-B buffer stores. Each lane
+//               ends up holding 32 contiguous outputs.
+//  * Numerics: X is split into two fp16 terms (~2^-21). C is one fp16 term (~2^-11 relative
+//    per bin, ~3e-4 relative on the layer output). Accumulation is fp32. This is inside the
+//    north star's 1e-3. bc_forward_mfma_kernel (bf16 hi/lo on both operands, ~1e-5) and
+//    bc_forward_valu_kernel (fp32) remain for callers that want more.
+//
+// Geometries (stat_eligible): b = 128 with K = 4096, and b = 64 with K = 2048 or 4096; any M.
+// DESIGN.md has the layouts, swizzles and the roofline accounting.
+#include "bcfft_device.h"
+
+namespace bcfft {
+
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+template <int B>
+struct GeoS {
+  static constexpr int H = B / 2;            // packed bins
+  static constexpr int L = H / 16;           // lanes per transform (16 points per lane)
+  static constexpr int BW = H / 8;           // bins per wave
+  static constexpr int NT = 2;               // 16-wide N-tiles per output group
+  static constexpr int NOG = STAT_OUT_BLOCKS;
+  static constexpr int TT = 4;               // tokens per M-tile (MFMA rows: 4 x re/im x hi/lo)
+  static constexpr int NW = 8, NTHR = 512;
+  static constexpr int REGION = 65536;       // x tile / A image / Y image
+  static constexpr int LOG2_2B = B == 128 ? 8 : 7;
+  // LDS tables behind the two regions
+  // lane-position tables use a 17-entry stride: the 4 (or 2) positions read by one instruction
+  // then sit in different banks
+  static constexpr int TS = 17;
+  static constexpr int TWF_OFF = 2 * REGION;                 // [L][TS] float2  W_H^(g k2)
+  static constexpr int TWI_OFF = TWF_OFF + L * TS * 8;       // [L][TS] float2  W_H^(-g k2)
+  static constexpr int UCO_OFF = TWI_OFF + L * TS * 8;       // [L][TS] float4  untangle
+  static constexpr int TWB_OFF = UCO_OFF + L * TS * 16;      // [B] float2      W_b^k
+  static constexpr int SLOT_OFF = TWB_OFF + B * 8;           // [2][4] uint     token max |x|
+  static constexpr int BIAS_OFF = SLOT_OFF + 32;             // [NOG * B] float  group's bias
+  static constexpr int LDS_BYTES = BIAS_OFF + NOG * B * 4;
+  static_assert(L == 2 || L == 4, "16 points per lane over 2 or 4 lanes");
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+};
+
+// lane position j of a transform -> k1 of the bins it owns after the cross-lane DFT
+template <int L>
+__device__ __forceinline__ int k1_of(int j) { return L == 4 ? ((j == 1) ? 2 : (j == 2) ? 1 : j) : j; }
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+constexpr int DPP_XOR1 = 0xB1;   // quad_perm [1,0,3,2]
+constexpr int DPP_XOR2 = 0x4E;   // quad_perm [2,3,0,1]
+constexpr int DPP_XOR3 = 0x1B;   // quad_perm [3,2,1,0]
+constexpr int DPP_P0 = 0xB4;     // quad_perm [0,1,3,2]
+
+// L-point DFT across the L lanes of a transform, for each of the 16 registers (four-step
+// step 3). Radix-2 DPP stages with lane-constant coefficients; lane j ends with bins
+// k1 = k1_of(j), stored as D_j^-1 (true) with D from stat_decode (signs / one rotation).
+template <int L, bool INV>
+__device__ __forceinline__ void lane_dft(float2 (&v)[16], int g) {
+  if constexpr (L == 2) {
+    const float s = g ? -1.f : 1.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const float px = dpp<DPP_XOR1>(v[k].x), py = dpp<DPP_XOR1>(v[k].y);
+      v[k].x = fmaf(s, px, v[k].x);
+      v[k].y = fmaf(s, py, v[k].y);
+    }
+  } else {
+    const float sa = g < 2 ? 1.f : -1.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {            // stage A: partner g ^ 2
+      const float px = dpp<DPP_XOR2>(v[k].x), py = dpp<DPP_XOR2>(v[k].y);
+      v[k].x = fmaf(sa, px, v[k].x);
+      v[k].y = fmaf(sa, py, v[k].y);
+    }
+    // stage B: partner g ^ 1; lanes 2,3 combine with -/+ i (forward / inverse)
+    const float al = g == 0 ? 1.f : (g == 1 ? -1.f : 0.f);
+    const float be = g < 2 ? 0.f : (INV ? -1.f : 1.f);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const float px = dpp<DPP_XOR1>(v[k].x), py = dpp<DPP_XOR1>(v[k].y);
+      const float nx = fmaf(be, py, fmaf(al, px, v[k].x));
+      const float ny = fmaf(-be, px, fmaf(al, py, v[k].y));
+      v[k].x = nx;
+      v[k].y = ny;
+    }
+  }
+}
+
+// decode matrix D_j (true = D * stored) after lane_dft, row-major {d00, d01, d10, d11}
+template <int L, bool INV>
+__host__ __device__ inline void stat_decode(int j, double d[4]) {
+  d[0] = 1; d[1] = 0; d[2] = 0; d[3] = 1;
+  if (L == 2) {
+    if (j == 1) { d[0] = -1; d[3] = -1; }
+  } else {
+    if (j == 1 || j == 2) { d[0] = -1; d[3] = -1; }
+    if (j == 3) {                                   // stored = i X (fwd) / -i X (inv)
+      d[0] = 0; d[3] = 0;
+      d[1] = INV ? -1 : 1;
+      d[2] = INV ? 1 : -1;
+    }
+  }
+}
+
+// v_mov through inline asm: the compiler cannot hoist or CSE what depends on it, so per-lane
+// addresses are rematerialised inside each phase instead of being kept (and spilled) across the
+// persistent loop next to the 128 VGPRs of stationary weights
+__device__ __forceinline__ int opaque(int v) {
+  int r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+
+// the forward storage of stat_decode<L, false> as a complex factor: true = sigma_j * stored
+template <int L>
+__host__ __device__ inline void stat_sigma(int j, double sg[2]) {
+  sg[0] = 1; sg[1] = 0;
+  if (j == 1 || (L == 4 && j == 2)) sg[0] = -1;
+  if (L == 4 && j == 3) { sg[0] = 0; sg[1] = -1; }
+}
+
+// output staging swizzle: 16-B piece p of a y row (lane position with bins k1 holds pieces
+// [k1 NQL, (k1+1) NQL)) -> unit p ^ f(k1) ^ par, conflict-free for the ds_write_b128 of a lane
+// group and the ds_read_b128 that re-reads rows in global order for 1-KiB stores
+template <int L, int NQL>
+__device__ __forceinline__ int y_unit(int p, int gi) {
+  const int k1 = p / NQL;
+  const int f = NQL == 8 ? (L == 4 ? ((k1 & 1) << 2 | (k1 & 2)) : 4 * k1) : (L == 4 ? 2 * (k1 >> 1) : 2 * k1);
+  return p ^ f ^ (gi & (L == 4 ? 1 : 3));
+}
+
+#ifdef BCFFT_MARKS
+#define MARK(n) asm volatile(";MARK " #n)
+#else
+#define MARK(n) do {} while (0)
+#endif
+
+// x staging swizzle (16-B units of a row) that keeps the forward DPP-group reads conflict-free
+template <int L, int ES>
+__device__ __forceinline__ int swz_x(int r) {
+  return ES == 4 ? (L == 4 ? 2 * (r & 7) : (r & 15)) : (r & 7);
+}
+
+template <int B, int KS, int XT, bool YF32>
+__global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
+    const void* __restrict__ xv, int64_t n_tokens, int n_out, const uint32_t* __restrict__ stat,
+    const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
+  using G = GeoS<B>;
+  constexpr int H = G::H, L = G::L, BW = G::BW, NT = G::NT, TT = G::TT, NW = G::NW;
+  constexpr int NI = 16 * KS, K = NI * B;
+  constexpr int ES = XTraits<XT>::ES;
+  constexpr int RB = B * ES;                       // x row bytes
+  constexpr int XTILE = TT * K * ES;
+  constexpr int RPWF = 64 / L;                     // forward rows per wave
+  constexpr int NDMA = RPWF * RB / 1024;           // LDS-DMA pieces per loading wave per M-tile
+  constexpr bool Y32 = YF32 || XT == BCFFT_F32;
+  constexpr int ESY = Y32 ? 4 : 2;
+  constexpr int NST = 32 * ESY / 16;               // 16-B stores per lane per M-tile
+  constexpr int NPIECE = BW * KS * NT;
+  constexpr int FWD_ROWS = TT * NI, INV_ROWS = TT * G::NOG;
+  static_assert(NDMA * 1024 == RPWF * RB && XTILE <= G::REGION, "x tile / DMA split");
+  static_assert(FWD_ROWS * L <= 512 && INV_ROWS * L <= 512, "one pass per phase");
+  static_assert(H * 32 * NI <= G::REGION && INV_ROWS * 8 * H <= G::REGION, "LDS images");
+  static_assert(NI / 4 >= 8, "A image swizzle needs >= 8 block quads per row");
+
+  ANALYSIS_INIT;
+  __shared__ __attribute__((aligned(16))) char lds[G::LDS_BYTES];
+  float2* twf = reinterpret_cast<float2*>(lds + G::TWF_OFF);
+  float2* twi = reinterpret_cast<float2*>(lds + G::TWI_OFF);
+  float4* uco = reinterpret_cast<float4*>(lds + G::UCO_OFF);
+  float2* twb = reinterpret_cast<float2*>(lds + G::TWB_OFF);
+  uint32_t* slots = reinterpret_cast<uint32_t*>(lds + G::SLOT_OFF);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp_o = blockIdx.y;                    // output group
+  const int64_t M = (int64_t)n_out * B;
+  const int64_t n_mtiles = (n_tokens + TT - 1) / TT;
+  const int gstride = gridDim.x;
+
+  // ---- tables (fp64 trig, once per workgroup)
+  for (int e = tid; e < L * 16; e += G::NTHR) {
+    const int g = e / 16, k2 = e % 16;
+    double sn, cs;
+    sincospi(2.0 * (double)((g * k2) % H) / (double)H, &sn, &cs);
+    twf[g * G::TS + k2] = make_float2((float)cs, (float)-sn);
+    twi[g * G::TS + k2] = make_float2((float)cs, (float)sn);
+    // forward untangle X'[k] = alpha Z[k] + beta conj(Z[H-k]) with alpha = (1+wi) - i wr,
+    // beta = (1-wi) + i wr (W^k = wr + i wi); bin 0: (2(a+b), 2(a-b)) = (2+2i) conj(Z0).
+    // Folded in: the lane_dft storage of this lane (sigma_g) and of the partner (sigma_gp).
+    const int k = k2 + 16 * k1_of<L>(g);
+    double ws, wc;
+    sincospi(2.0 * (double)k / (double)B, &ws, &wc);
+    const double wr = wc, wi = -ws;
+    double ar = 1 + wi, ai = -wr, br = 1 - wi, bi = wr;
+    if (k == 0) { ar = 0; ai = 0; br = 2; bi = 2; }
+    int gp;                                        // partner lane of bin H - k
+    if (k2 == 0) gp = (L == 4) ? (g < 2 ? g : g ^ 1) : g;
+    else gp = (L == 4) ? (g ^ 3) : (g ^ 1);
+    double sg[2], sp[2];                           // true = sigma * stored
+    stat_sigma<L>(g, sg);
+    stat_sigma<L>(gp, sp);
+    uco[g * G::TS + k2] = make_float4((float)(ar * sg[0] - ai * sg[1]), (float)(ar * sg[1] + ai * sg[0]),   // alpha sigma_g
+                         (float)(br * sp[0] + bi * sp[1]), (float)(bi * sp[0] - br * sp[1]));  // beta conj(sigma_gp)
+  }
+  for (int k = tid; k < B; k += G::NTHR) {
+    double sn, cs;
+    sincospi(2.0 * (double)k / (double)B, &sn, &cs);
+    twb[k] = make_float2((float)cs, (float)-sn);
+  }
+  if (tid < 8) slots[tid] = 0u;
+  // the group's bias as fp32 in LDS, so no VMEM load sits in the loop: a waited load would
+  // also drain every older y store and x DMA (vmcnt retires in order)
+  float* bias_l = reinterpret_cast<float*>(lds + G::BIAS_OFF);
+  if (bias_dt != BCFFT_NONE) {
+    for (int e = tid; e < G::NOG * B; e += G::NTHR) {
+      const int64_t col = (int64_t)grp_o * G::NOG * B + e;
+      bias_l[e] = col < (int64_t)n_out * B ? load_scalar(bias, col, bias_dt) : 0.f;
+    }
+  }
+  lds_barrier();                                   // tables before the weight loads (pressure)
+
+  // ---- stationary B fragments: conj(C) * s_C as fp16, K/32 VGPRs per lane
+  const float inv_sc = __uint_as_float(stat[1]);
+  f16x8 creg[BW][KS][NT];
+  {
+    const uint4* img = reinterpret_cast<const uint4*>(stat + 4) + ((int64_t)(grp_o * NW + wave) * NPIECE) * 64 + lane;
+#pragma unroll
+    for (int fb = 0; fb < BW; ++fb)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          creg[fb][ks][nt] = __builtin_bit_cast(f16x8, img[((fb * KS + ks) * NT + nt) * 64]);
+  }
+
+  // ---- x M-tile -> region by LDS-DMA. Each wave loads exactly the x rows its own forward
+  // groups transform (RPWF rows = NDMA 1-KiB pieces), so its own vmcnt wait is all it needs
+  // before reading them. The tile's 4 token rows are one contiguous span of x: a lane's source
+  // offset is its LDS byte with the row's unit swizzle (swz_x) XORed in; the buffer range check
+  // zero-fills rows past n_tokens (those tokens are never stored).
+  auto dma_tile = [&](int64_t m, char* region) {
+    if (wave >= FWD_ROWS / RPWF) return;
+    const int64_t tok0 = m * TT;
+    const int64_t ntok = n_tokens - tok0 < TT ? n_tokens - tok0 : TT;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>((const char*)xv) + tok0 * K * ES, 0, (int)(ntok * K * ES), 0x00020000);
+    const int dlane = opaque(lane);
+#pragma unroll
+    for (int q = 0; q < NDMA; ++q) {
+      const int c = wave * NDMA + q;
+      const int byte = c * 1024 + dlane * 16;
+      const int voff = byte ^ (swz_x<L, ES>(byte / RB) << 4);
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(region + c * 1024));
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(voff), "s"(xrs), "s"(dst) : "memory");
+    }
+  };
+
+  // Y image, bin-pair-major: the 16-B unit of bins (2p, 2p+1) of row R = t*NOG + o sits at
+  // p*PS + 16 * (R ^ (p & 15)). PS = 2 A-image bins, so the pairs of wave w's bins cover exactly
+  // the A-image bytes of those bins: each wave overwrites only what it alone has read.
+  constexpr int PS = 2 * 32 * NI;
+  auto yunit = [](int p, int R) { return p * PS + 16 * (R ^ (p & 15)); };
+  // inverse rows: group grp -> (t, o); a half-wave's 8 rows differ in bits 1-3 of R
+  auto inv_row = [](int gr, int& t, int& o) {
+    const int w = gr >> 4, h = (gr >> 3) & 1, r8 = gr & 7;
+    t = w >> 1;
+    o = 16 * (w & 1) + 2 * r8 + h;
+  };
+  // y staging: piece pc (16 B) of row R -> bin-pair unit spc(pc) of that row (conflict-free
+  // ds_write_b128 from the lane groups and ds_read_b128 in global order for fp32 b = 128)
+  constexpr int NQL = 32 * ESY / 16;                // 16-B pieces of y per lane
+  constexpr int NPR = B * ESY / 16;                 // 16-B pieces per y row
+  constexpr int RPI = 64 / NPR;                     // rows per store instruction
+  auto spc = [](int pc) {
+    if constexpr (NQL == 8 && L == 4) {
+      const int k1 = pc >> 3, q = pc & 7;
+      return (k1 & 1) | ((q & 1) << 1) | ((k1 >> 1) << 2) | ((q >> 1) << 3);
+    } else {
+      return pc;
+    }
+  };
+  // the wave stores the rows it staged (P4 of tile mt), RPI whole rows per 1-KiB instruction
+  auto store_tile = [&](int64_t mt, const char* regn) {
+    if (wave * 64 / L >= INV_ROWS) return;
+    const int64_t stok0 = mt * TT;
+    const int64_t ntok = n_tokens - stok0 < TT ? n_tokens - stok0 : TT;
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (char*)yv + stok0 * M * ESY, 0, (int)(ntok * M * ESY), 0x00020000);
+    const int slane = opaque(lane);
+#pragma unroll
+    for (int q = 0; q < NST; ++q) {
+      const int gi = q * RPI + slane / NPR, pc = slane % NPR;
+      int st_t, st_o;
+      inv_row(wave * (64 / L) + gi, st_t, st_o);
+      const int sog = grp_o * G::NOG + st_o;
+      const uint4 d = *reinterpret_cast<const uint4*>(regn + yunit(spc(pc), st_t * G::NOG + st_o));
+      const int yoff = sog < n_out ? (int)(((int64_t)st_t * M + (int64_t)sog * B) * ESY + 16 * pc) : 0x7fff0000;
+      if (!ABLATE(2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d), yrs, yoff, 0, 0);
+    }
+  };
+
+  // Pipeline per tile m (regions R = R[it & 1], R' = the other), three barriers:
+  //   own x rows landed (vmcnt) | forward FFT + untangle, token max -> LDS | B1 | scale, split ->
+  //   A image in place; stores of tile m-1 from R' | B2 | DMA x(m+1) -> R', MFMAs, own Y pairs
+  //   over own A bins | B4 | inverse, y staged into own Y rows (stored during tile m+1)
+  int64_t m = blockIdx.x;
+  STAMP(0);
+  if (m < n_mtiles && !ABLATE(16)) dma_tile(m, lds);
+
+  int it = 0;
+  for (; m < n_mtiles; ++it, m += gstride) {
+    char* region = lds + (it & 1) * G::REGION;
+    char* other = lds + ((it + 1) & 1) * G::REGION;
+    uint32_t* slot = slots + (it & 1) * 4;
+    const bool more = m + gstride < n_mtiles;
+    const int sb = 1 + 7 * (it & 7);
+    STAMP(sb);
+    wait_vmcnt<0>();                                // this wave's x rows (its youngest VMEM ops)
+    STAMP(sb + 1);
+
+    // ---- forward: x rows -> X' (untangled, packed) in registers; token max |X'| -> slot
+    const bool fwd_active = wave * 64 / L < FWD_ROWS;
+    const bool inv_active = wave * 64 / L < INV_ROWS;
+    float2 v[16];
+    float2 xs[16];
+    if (fwd_active) {
+      const int ptid = opaque(tid);
+      const int grp = ptid / L, g = ptid % L;
+      const int frow = grp < FWD_ROWS ? grp : 0;
+      const int ft = frow / NI;
+      const char* rowp = region + frow * RB;
+#pragma unroll
+      for (int n2 = 0; n2 < 16; ++n2) {
+        const int n = g + L * n2;
+        if constexpr (ES == 4) {
+          const int off = 8 * n;
+          v[n2] = *reinterpret_cast<const float2*>(rowp + (((off >> 4) ^ swz_x<L, ES>(frow)) << 4) + (off & 15));
+        } else {
+          const int off = 4 * n;
+          const uint32_t w = *reinterpret_cast<const uint32_t*>(rowp + (((off >> 4) ^ swz_x<L, ES>(frow)) << 4) + (off & 15));
+          v[n2] = XT == BCFFT_BF16 ? make_float2(bf16_to_f32(w & 0xffffu), bf16_to_f32(w >> 16))
+                                   : make_float2(f16_to_f32(w & 0xffffu), f16_to_f32(w >> 16));
+        }
+      }
+      float2 tw[16];                                // four-step twiddles, issued ahead of the DFT
+#pragma unroll
+      for (int k2 = 1; k2 < 16; ++k2) tw[k2] = twf[g * G::TS + k2];
+      float4 uc[16];
+      if (!ABLATE(4)) {
+        dft<16, false>(v);
+#pragma unroll
+        for (int k2 = 1; k2 < 16; ++k2) v[k2] = cmul(v[k2], tw[k2]);
+      }
+#pragma unroll
+      for (int k2 = 0; k2 < 8; ++k2) uc[k2] = uco[g * G::TS + k2];   // in flight under lane_dft
+      __builtin_amdgcn_sched_barrier(0);
+      if (!ABLATE(4)) lane_dft<L, false>(v, g);
+      // untangle X'[k] = alpha s + beta conj(p), partner bin H - k by DPP
+      float mx = 0.f;
+#pragma unroll
+      for (int k2 = 0; k2 < 16; ++k2) {
+        if (k2 == 4) {                              // second half of the coefficients
+#pragma unroll
+          for (int kk = 8; kk < 16; ++kk) uc[kk] = uco[g * G::TS + kk];
+        }
+        const int src = k2 == 0 ? 0 : 16 - k2;
+        float px, py;
+        if constexpr (L == 4) {
+          if (k2 == 0) { px = dpp<DPP_P0>(v[0].x); py = dpp<DPP_P0>(v[0].y); }
+          else { px = dpp<DPP_XOR3>(v[src].x); py = dpp<DPP_XOR3>(v[src].y); }
+        } else {
+          if (k2 == 0) { px = v[0].x; py = v[0].y; }
+          else { px = dpp<DPP_XOR1>(v[src].x); py = dpp<DPP_XOR1>(v[src].y); }
+        }
+        const float4 c = uc[k2];
+        xs[k2].x = fmaf(c.x, v[k2].x, fmaf(-c.y, v[k2].y, fmaf(c.z, px, c.w * py)));
+        xs[k2].y = fmaf(c.x, v[k2].y, fmaf(c.y, v[k2].x, fmaf(c.w, px, -c.z * py)));
+        mx = fmaxf(mx, fmaxf(fabsf(xs[k2].x), fabsf(xs[k2].y)));
+      }
+      mx = fmaxf(mx, dpp<DPP_XOR1>(mx));
+      if constexpr (L == 4) mx = fmaxf(mx, dpp<DPP_XOR2>(mx));
+      if (g == 0 && grp < FWD_ROWS) atomicMax(&slot[ft], __float_as_uint(mx));
+    }
+    lds_barrier();                                  // B1: every x row read, token maxima posted
+    STAMP(sb + 2);
+    if (tid < 4) slots[((it + 1) & 1) * 4 + tid] = 0u;   // next tile's maxima
+    if (fwd_active) {
+      const int ptid = opaque(tid);
+      const int grp = ptid / L, g = ptid % L;
+      const int k1 = k1_of<L>(g);
+      const int frow = grp < FWD_ROWS ? grp : 0;
+      const int ft = frow / NI, fi = frow % NI;
+      // s_t = 2^(15 - E), max |X'| < 2^E over the token: X' s_t fits fp16 with headroom
+      const int e_t = __builtin_amdgcn_frexp_expf(__uint_as_float(slot[ft]));
+      int nsc = 15 - e_t;
+      nsc = nsc < -126 ? -126 : (nsc > 127 ? 127 : nsc);
+      const float s_t = __int_as_float((nsc + 127) << 23);
+      char* aimg = region;
+      const int hf = k1 * (8 / L);
+#pragma unroll
+      for (int k2 = 0; k2 < 16; ++k2) {
+        const float ox = xs[k2].x * s_t, oy = xs[k2].y * s_t;
+        const f16x2 hi = __builtin_bit_cast(f16x2, __builtin_amdgcn_cvt_pkrtz(ox, oy));
+        const f16x2 lo = __builtin_bit_cast(f16x2, __builtin_amdgcn_cvt_pkrtz(ox - (float)hi.x, oy - (float)hi.y));
+        const int f = k2 + 16 * k1;
+        if (grp < FWD_ROWS) {
+          char* base = aimg + f * (32 * NI);
+          const int j0 = 2 * ft, j1 = 2 * ft + 1;
+          *reinterpret_cast<f16x2*>(base + j0 * (4 * NI) + 16 * (((fi >> 2) ^ j0 ^ hf)) + 4 * (fi & 3)) = hi;
+          *reinterpret_cast<f16x2*>(base + j1 * (4 * NI) + 16 * (((fi >> 2) ^ j1 ^ hf)) + 4 * (fi & 3)) = lo;
+        }
+      }
+    }
+    if (it > 0) store_tile(m - gstride, other);     // tile m-1's y, staged in R'
+    lds_barrier();                                  // B2: A image complete; R' staging read
+    STAMP(sb + 3);
+    if (more && !ABLATE(16)) dma_tile(m + gstride, other);
+
+    // ---- per-bin complex MAC on the matrix cores; results overwrite this wave's own A bins
+    {
+      const int mlane = opaque(lane);
+      const int arow = mlane & 15, kb = mlane >> 4;  // A row (token, re/im, hi/lo), K quad
+      const int a_t = arow >> 2, a_reim = (arow >> 1) & 1, a_prec = arow & 1;
+      const int a_j = 2 * a_t + a_prec;
+      const uint32_t a_sel = a_reim ? 0x01000302u : 0x03020100u;   // im rows: (re, im) -> (im, -re)
+      const uint32_t a_xor = a_reim ? 0x80000000u : 0u;
+      const uint32_t a_bin0 = a_reim ? 0xffff0000u : 0x0000ffffu;  // bin 0: (X0, 0) / (0, X_H)
+      char* aimg = region;
+      uint4 araw[BW][KS];                           // every A fragment of the wave's bins, read
+#pragma unroll                                       // before the first MFMA
+      for (int fb = 0; fb < BW; ++fb) {
+        const int f = wave * BW + fb;
+        const int hf = (f >> 4) * (8 / L);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+          araw[fb][ks] = ABLATE(32) ? make_uint4(a_j, kb, f, ks)
+                                    : *reinterpret_cast<const uint4*>(aimg + f * (32 * NI) + a_j * (4 * NI) + 16 * ((4 * ks + kb) ^ a_j ^ hf));
+      }
+      float2 ybuf[BW][NT];
+#pragma unroll
+      for (int fb = 0; fb < BW; ++fb) {
+        const int f = wave * BW + fb;
+        f32x4 acc[NT];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          uint4 raw = araw[fb][ks];
+          if (ABLATE(64)) {
+          } else if (f == 0) {
+            raw.x &= a_bin0; raw.y &= a_bin0; raw.z &= a_bin0; raw.w &= a_bin0;
+          } else {
+            raw.x = __builtin_amdgcn_perm(raw.x, raw.x, a_sel) ^ a_xor;
+            raw.y = __builtin_amdgcn_perm(raw.y, raw.y, a_sel) ^ a_xor;
+            raw.z = __builtin_amdgcn_perm(raw.z, raw.z, a_sel) ^ a_xor;
+            raw.w = __builtin_amdgcn_perm(raw.w, raw.w, a_sel) ^ a_xor;
+          }
+          const f16x8 a = __builtin_bit_cast(f16x8, raw);
+          if (ABLATE(1)) {
+            asm volatile("" :: "v"(raw.x));
+            continue;
+          }
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, creg[fb][ks][nt], acc[nt], 0, 0, 0);
+        }
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)            // rows 4t + {re hi, re lo, im hi, im lo}
+          ybuf[fb][nt] = make_float2(acc[nt][0] + acc[nt][1], acc[nt][2] + acc[nt][3]);
+      }
+      // own A bins were all read (wave-local DS order): Y pairs go over them, 16 B per lane
+      wave_lds_sync();
+      const int yt = mlane >> 4;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int R = yt * G::NOG + nt * 16 + (mlane & 15);
+#pragma unroll
+        for (int fp = 0; fp < BW / 2; ++fp) {
+          const int pr = (wave * BW) / 2 + fp;
+          *reinterpret_cast<float4*>(aimg + yunit(pr, R)) =
+              make_float4(ybuf[2 * fp][nt].x, ybuf[2 * fp][nt].y, ybuf[2 * fp + 1][nt].x, ybuf[2 * fp + 1][nt].y);
+        }
+      }
+    }
+    STAMP(sb + 4);
+    lds_barrier();                                  // B4: Y image complete
+    STAMP(sb + 5);
+
+    // ---- inverse transforms -> y rows staged in this tile's region (stored next tile)
+    if (inv_active) {
+      const int ptid = opaque(tid);
+      const int grp = ptid / L, g = ptid % L;
+      const int k1 = k1_of<L>(g);
+      int inv_t, inv_o;
+      inv_row(grp, inv_t, inv_o);
+      const int R = inv_t * G::NOG + inv_o;
+      float2 yk[16], yh[16], wk[16];
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb) {
+#pragma unroll
+      for (int n2 = 8 * hb; n2 < 8 * hb + 8; ++n2) {
+        const int k = g + L * n2, kh = (H - k) & (H - 1);
+        yk[n2] = *reinterpret_cast<const float2*>(region + yunit(k >> 1, R) + 8 * (k & 1));
+        yh[n2] = *reinterpret_cast<const float2*>(region + yunit(kh >> 1, R) + 8 * (kh & 1));
+        wk[n2] = twb[k];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int n2 = 8 * hb; n2 < 8 * hb + 8; ++n2) {
+        const int k = g + L * n2;
+        const float er = yk[n2].x + yh[n2].x, ei = yk[n2].y - yh[n2].y;   // E = Y[k] + conj(Y[H-k])
+        const float dr = yk[n2].x - yh[n2].x, di = yk[n2].y + yh[n2].y;   // D = Y[k] - conj(Y[H-k])
+        const float2 w = wk[n2];                                          // Zi = E + i D conj(W^k)
+        float2 z;
+        z.x = er - (di * w.x - dr * w.y);
+        z.y = ei + (dr * w.x + di * w.y);
+        if (k == 0) z = make_float2(yk[n2].x + yk[n2].y, yk[n2].x - yk[n2].y);   // packed bin 0
+        v[n2] = z;
+      }
+      }
+      float2 tw[16];
+#pragma unroll
+      for (int k2 = 1; k2 < 16; ++k2) tw[k2] = twi[g * G::TS + k2];
+      if (!ABLATE(8)) {
+        dft<16, true>(v);
+#pragma unroll
+        for (int k2 = 1; k2 < 16; ++k2) v[k2] = cmul(v[k2], tw[k2]);
+        lane_dft<L, true>(v, g);
+      }
+      // y[32 k1 + 2 k2 + {0,1}] = D (R0, R1) / (s_t s_C), D = stat_decode<L, true>(g)
+      const int e_t = __builtin_amdgcn_frexp_expf(__uint_as_float(slot[inv_t]));
+      int nsc = 15 - e_t;
+      nsc = nsc < -126 ? -126 : (nsc > 127 ? 127 : nsc);
+      const float sc = __int_as_float((127 - nsc) << 23) * inv_sc;
+      const bool rot = L == 4 && g == 3;                     // stored = -i z
+      const float sd = (g == 1 || g == 2) ? -sc : sc;
+      const float c00 = rot ? 0.f : sd, c01 = rot ? -sc : 0.f;
+      const float c10 = rot ? sc : 0.f, c11 = rot ? 0.f : sd;
+      const float* brow = bias_l + inv_o * B + 32 * k1;
+      wave_lds_sync();                               // this group's Y reads precede its y writes
+      // 8 outputs (4 registers) per step: .to(x.dtype) :266, + bias :270-271, .to(y dtype)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float o8[8];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const float2 z = v[4 * q + h];
+          o8[2 * h] = round_to(fmaf(c00, z.x, c01 * z.y), XT);
+          o8[2 * h + 1] = round_to(fmaf(c10, z.x, c11 * z.y), XT);
+        }
+        if (bias_dt != BCFFT_NONE) {
+          const float4 b0 = *reinterpret_cast<const float4*>(brow + 8 * q);
+          const float4 b1 = *reinterpret_cast<const float4*>(brow + 8 * q + 4);
+          o8[0] += b0.x; o8[1] += b0.y; o8[2] += b0.z; o8[3] += b0.w;
+          o8[4] += b1.x; o8[5] += b1.y; o8[6] += b1.z; o8[7] += b1.w;
+        }
+        if constexpr (Y32) {
+#pragma unroll
+          for (int hq = 0; hq < 2; ++hq) {
+            const int pc = k1 * NQL + 2 * q + hq;
+            *reinterpret_cast<float4*>(region + yunit(spc(pc), R)) =
+                make_float4(o8[4 * hq], o8[4 * hq + 1], o8[4 * hq + 2], o8[4 * hq + 3]);
+          }
+        } else {
+          uint32_t hh[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) hh[e] = XT == BCFFT_BF16 ? f32_to_bf16(o8[e]) : f32_to_f16(o8[e]);
+          const int pc = k1 * NQL + q;
+          *reinterpret_cast<uint4*>(region + yunit(spc(pc), R)) =
+              make_uint4(hh[0] | (hh[1] << 16), hh[2] | (hh[3] << 16), hh[4] | (hh[5] << 16), hh[6] | (hh[7] << 16));
+        }
+      }
+    }
+    STAMP(sb + 6);
+  }
+  // the last tile's stores (each wave its own staged rows: wave-local LDS order suffices)
+  if (it > 0) {
+    wave_lds_sync();
+    store_tile(m - gstride, lds + ((it + 1) & 1) * G::REGION);
+  }
+  STAMP(63);
+}
+
+// ================================================================== weight preparation
+// s_C = 2^(15 - E), max |S| < 2^E over the packed spectra; header {s_C, 1/s_C}
+template <int B>
+__global__ void bc_stat_scale_kernel(int n_out, int n_in, float2* __restrict__ spec) {
+  const SpecLayout sl = spec_layout(n_out, n_in, B);
+  const float* p = reinterpret_cast<const float*>(spec);
+  const int64_t n = sl.packed_f2 * 2;
+  float mx = 0.f;
+  for (int64_t e = threadIdx.x; e < n; e += blockDim.x) mx = fmaxf(mx, fabsf(p[e]));
+  __shared__ float red[1024];
+  red[threadIdx.x] = mx;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const int e = __builtin_amdgcn_frexp_expf(red[0]);
+    int n2 = 15 - e;
+    n2 = n2 < -126 ? -126 : (n2 > 127 ? 127 : n2);
+    uint32_t* hdr = reinterpret_cast<uint32_t*>(spec) + sl.stat_off_u32;
+    hdr[0] = (uint32_t)((n2 + 127) << 23);
+    hdr[1] = (uint32_t)((127 - n2) << 23);
+    hdr[2] = 0u;
+    hdr[3] = 0u;
+  }
+}
+
+// one thread per (group, wave, piece, lane) 16-B fragment: 4 input blocks x (re, im) fp16 of
+// conj(S) * s_C (bin 0: (S_0, S_H) * s_C), zero outside the operator
+template <int B>
+__global__ void bc_stat_image_kernel(int n_out, int n_in, float2* __restrict__ spec) {
+  constexpr int H = B / 2, BW = H / 8, NT = 2, NW = 8;
+  const SpecLayout sl = spec_layout(n_out, n_in, B);
+  const int ks_n = n_in / 16;
+  const int npiece = sl.stat_pieces;
+  const int64_t total = (int64_t)sl.stat_groups * NW * npiece * 64;
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(spec) + sl.stat_off_u32;
+  uint4* img = reinterpret_cast<uint4*>(hdr + 4);
+  const float sc = __uint_as_float(hdr[0]);
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(idx & 63);
+    const int64_t rest = idx >> 6;
+    const int p = (int)(rest % npiece);
+    const int w = (int)((rest / npiece) % NW);
+    const int gq = (int)(rest / npiece / NW);
+    const int nt = p % NT, ks = (p / NT) % ks_n, fb = p / NT / ks_n;
+    const int f = w * BW + fb;
+    const int o = gq * STAT_OUT_BLOCKS + nt * 16 + (lane & 15);
+    const int i0 = ks * 16 + 4 * (lane >> 4);
+    uint32_t d[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int i = i0 + e;
+      float2 c = make_float2(0.f, 0.f);
+      if (o < n_out && i < n_in) {
+        c = spec[((int64_t)o * n_in + i) * H + f];
+        if (f != 0) c.y = -c.y;
+      }
+      const f16x2 h = {(_Float16)(c.x * sc), (_Float16)(c.y * sc)};
+      d[e] = __builtin_bit_cast(uint32_t, h);
+    }
+    img[idx] = make_uint4(d[0], d[1], d[2], d[3]);
+  }
+}
+
+}  // namespace bcfft
+
+namespace {
+int g_cu_count = 0;
+int cu_count() {
+  if (g_cu_count <= 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      g_cu_count = n;
+    else
+      g_cu_count = 256;
+  }
+  return g_cu_count;
+}
+
+template <int B, int KS, int XT, bool YF32>
+void launch_stat(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt,
+                 void* y, hipStream_t s) {
+  const bcfft::SpecLayout sl = bcfft::spec_layout(n_out, 16 * KS, B);
+  const int groups = sl.stat_groups;
+  // one workgroup per CU; the groups of one token slice share an XCD (stride multiple of 8)
+  int gx = cu_count() / groups;
+  if (gx >= 8) gx -= gx % 8;
+  if (gx < 1) gx = 1;
+  const int64_t n_mtiles = (n + 3) / 4;
+  if (gx > n_mtiles) gx = (int)n_mtiles;
+  const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
+  hipLaunchKernelGGL((bcfft::bc_forward_stat_kernel<B, KS, XT, YF32>), dim3(gx, groups), dim3(512), 0, s,
+                     x, n, n_out, stat, bias, bias_dt, y);
+}
+
+template <int B, int KS>
+bool launch_stat_dt(int xdt, bool yf32, const void* x, int64_t n, int n_out, const void* spec,
+                    const void* bias, int bias_dt, void* y, hipStream_t s) {
+  if (xdt == BCFFT_F32) launch_stat<B, KS, BCFFT_F32, true>(x, n, n_out, spec, bias, bias_dt, y, s);
+  else if (xdt == BCFFT_F16 && yf32) launch_stat<B, KS, BCFFT_F16, true>(x, n, n_out, spec, bias, bias_dt, y, s);
+  else if (xdt == BCFFT_F16) launch_stat<B, KS, BCFFT_F16, false>(x, n, n_out, spec, bias, bias_dt, y, s);
+  else if (yf32) launch_stat<B, KS, BCFFT_BF16, true>(x, n, n_out, spec, bias, bias_dt, y, s);
+  else launch_stat<B, KS, BCFFT_BF16, false>(x, n, n_out, spec, bias, bias_dt, y, s);
+  return true;
+}
+}  // namespace
+
+namespace bcfft {
+bool launch_forward_stat(int b, int n_in, int xdt, bool yf32, const void* x, int64_t n, int n_out,
+                         const void* spec, const void* bias, int bias_dt, void* y, hipStream_t s) {
+  if (!stat_eligible(n_in, b)) return false;
+  if (b == 128) return launch_stat_dt<128, 2>(xdt, yf32, x, n, n_out, spec, bias, bias_dt, y, s);
+  if (n_in == 64) return launch_stat_dt<64, 4>(xdt, yf32, x, n, n_out, spec, bias, bias_dt, y, s);
+  return launch_stat_dt<64, 2>(xdt, yf32, x, n, n_out, spec, bias, bias_dt, y, s);
+}
+
+void launch_stat_image(int b, int n_out, int n_in, void* spec, hipStream_t s) {
+  if (!stat_eligible(n_in, b)) return;
+  const SpecLayout sl = spec_layout(n_out, n_in, b);
+  const int64_t total = (int64_t)sl.stat_groups * 8 * sl.stat_pieces * 64;
+  const unsigned blocks = (unsigned)((total + 255) / 256 < 65535 ? (total + 255) / 256 : 65535);
+  if (b == 128) {
+    hipLaunchKernelGGL(bc_stat_scale_kernel<128>, dim3(1), dim3(1024), 0, s, n_out, n_in, (float2*)spec);
+    hipLaunchKernelGGL(bc_stat_image_kernel<128>, dim3(blocks), dim3(256), 0, s, n_out, n_in, (float2*)spec);
+  } else {
+    hipLaunchKernelGGL(bc_stat_scale_kernel<64>, dim3(1), dim3(1024), 0, s, n_out, n_in, (float2*)spec);
+    hipLaunchKernelGGL(bc_stat_image_kernel<64>, dim3(blocks), dim3(256), 0, s, n_out, n_in, (float2*)spec);
+  }
+}
+}  // namespace bcfft
+
+#ifdef BCFFT_ABLATE
+// analysis build only: switches / stamp buffer of bc_forward_stat_kernel (this TU's copies).
+// 1 skip MFMAs, 2 skip y stores, 4 skip forward FFT math, 8 skip inverse FFT math, 16 skip x DMA,
+// 32 skip A-fragment LDS reads, 64 skip the A im-row transform
+extern "C" int bcfft_set_ablation_stat(int flags) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(bcfft::g_ablate), &flags, sizeof(int)) == hipSuccess ? 0 : BCFFT_ERR_HIP;
+}
+// stamp slots per wave: 0 start | per M-tile it (base 1 + 7 (it % 8)): +0 loop top, +1 own x
+// landed, +2 after B1, +3 after B2, +4 MFMAs + Y pairs done, +5 after B4, +6 inverse done | 63 end
+extern "C" int bcfft_set_stamps_stat(void* buf) {
+  unsigned long long* p = (unsigned long long*)buf;
+  return hipMemcpyToSymbol(HIP_SYMBOL(bcfft::g_stamps), &p, sizeof(p)) == hipSuccess ? 0 : BCFFT_ERR_HIP;
+}
+#endif

@@ -1,0 +1,147 @@
+"""GPU parity of the stationary-weight kernel (BCFFT_ALGO=stationary, the AUTO choice for
+b = 128 / K = 4096 and b = 64 / K in {2048, 4096}) against the CPU oracle.
+
+The kernel keeps the weight spectra as one fp16 term (~2^-11 relative per bin) and splits X
+into two fp16 terms under a per-token power-of-two scale. Tolerance: the north star's 1e-3
+relative Frobenius error on fp32 outputs. Measured parity is ~3e-4; the tests assert < 6e-4 so
+that a regression shows up long before the contract is at risk. 16-bit outputs compare the
+rounded values within one output ulp plus the same norm bound."""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import rel_err
+from oracle import bc_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TDT = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16}
+ODT = {"float32": O.F32, "float16": O.F16, "bfloat16": O.BF16}
+STAT_TOL = 6e-4
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    import bcfft
+    bcfft.load()
+    return torch.device("cuda:0")
+
+
+def _run(dev, x, c, bv, xdt, mdt, algo="stationary"):
+    from bcfft import ops
+    xt = torch.from_numpy(x).to(dev).to(TDT[xdt])
+    ct = torch.from_numpy(c).to(dev).to(TDT[mdt])
+    bt = torch.from_numpy(bv).to(dev).to(TDT[mdt]) if bv is not None else None
+    spec = ops.spectra(ct)
+    b = c.shape[-1]
+    y = ops.forward(xt, spec, bt, b, c.shape[0] * b, algo=algo)
+    torch.cuda.synchronize()
+    c_eff = O.round_to(c, ODT[mdt])
+    b_eff = O.round_to(bv, ODT[mdt]) if bv is not None else None
+    ref = O.bc_forward(O.round_to(x, ODT[xdt]), c_eff, b_eff, x_dtype=ODT[xdt],
+                       bias_dtype=ODT[mdt] if bv is not None else None)
+    return y, ref
+
+
+def _check(y, ref, xdt="float32"):
+    g = y.detach().float().cpu().numpy()
+    assert g.shape == ref.shape
+    assert np.isfinite(g).all()
+    e = rel_err(g, ref)
+    rdt = y.dtype if xdt == "float32" else TDT[xdt]      # y = round_x(...) + bias (:266-271)
+    if rdt != torch.float32:
+        ulp = 2.0 ** -7 if rdt == torch.bfloat16 else 2.0 ** -10
+        rms = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
+        bad = np.abs(g - ref) > 2 * ulp * np.abs(ref) + 2 * ulp * rms
+        assert not bad.any(), f"{int(bad.sum())} elements beyond ~1 ulp"
+        assert e < 4e-3, e
+    else:
+        assert e < STAT_TOL, f"rel err {e:.3e}"
+    return e
+
+
+CASES = [
+    # (K, M, b, N, x dtype, module dtype, bias)
+    (4096, 4096, 128, 1, "float32", "float32", True),      # one token: partial M-tile
+    (4096, 4096, 128, 4, "float32", "float32", False),
+    (4096, 4096, 128, 37, "float32", "float32", True),
+    (4096, 4096, 128, 301, "bfloat16", "bfloat16", False),  # 76 M-tiles, ragged
+    (4096, 4096, 128, 64, "float16", "float16", True),
+    (4096, 4096, 128, 50, "bfloat16", "float32", True),     # promotion -> fp32 output
+    (4096, 11008, 128, 31, "bfloat16", "bfloat16", False),  # 3 output groups, last one partial
+    (4096, 11008, 128, 9, "float32", "float32", True),
+    (4096, 4096, 64, 15, "float32", "float32", True),       # b = 64, K-steps 4, 2 groups
+    (4096, 4096, 64, 40, "bfloat16", "bfloat16", False),
+    (2048, 1024, 64, 9, "float32", "float32", True),        # b = 64, K-steps 2, 1 group
+    (2048, 3072, 64, 23, "float16", "float32", False),
+]
+
+
+@pytest.mark.parametrize("k,m,b,n,xdt,mdt,bias", CASES)
+def test_stationary_vs_oracle(dev, k, m, b, n, xdt, mdt, bias):
+    rng = np.random.default_rng(k + 3 * m + 7 * b + n)
+    c = (rng.standard_normal((m // b, k // b, b)) * 0.01).astype(np.float32)
+    bv = (rng.standard_normal(m) * 0.1).astype(np.float32) if bias else None
+    x = rng.standard_normal((n, k)).astype(np.float32)
+    y, ref = _run(dev, x, c, bv, xdt, mdt)
+    _check(y, ref, xdt)
+
+
+def test_stationary_is_auto_for_eligible_shapes(dev):
+    """AUTO picks the stationary kernel at 4096^2 b=128: same bits as algo=stationary."""
+    rng = np.random.default_rng(1)
+    c = (rng.standard_normal((32, 32, 128)) * 0.01).astype(np.float32)
+    x = rng.standard_normal((12, 4096)).astype(np.float32)
+    ya, _ = _run(dev, x, c, None, "float32", "float32", algo="auto")
+    ys, _ = _run(dev, x, c, None, "float32", "float32", algo="stationary")
+    assert torch.equal(ya, ys)
+
+
+def test_stationary_per_token_scale(dev):
+    """Tokens 10^9 apart in magnitude, zero tokens and a massive-activation channel: the
+    per-token power-of-two scale keeps every token inside fp16 range at full relative accuracy."""
+    rng = np.random.default_rng(2)
+    c = (rng.standard_normal((32, 32, 128)) * 0.01).astype(np.float32)
+    x = rng.standard_normal((9, 4096)).astype(np.float32)
+    x[0] *= 1e4
+    x[1] *= 1e-5
+    x[2] = 0.0
+    x[3, 77] = 3000.0                     # one massive channel beside unit-scale ones
+    x[5] *= 1e-30                         # far below fp16's range without the scale
+    y, ref = _run(dev, x, c, None, "float32", "float32")
+    g = y.cpu().numpy()
+    assert np.all(g[2] == 0.0)
+    for t in (0, 1, 3, 4, 5, 6):
+        e = rel_err(g[t], ref[t])
+        assert e < STAT_TOL, (t, e)
+
+
+def test_stationary_rejects_ineligible_geometry(dev):
+    from bcfft import ops
+    c = torch.zeros(4, 4, 128, device=dev)
+    spec = ops.spectra(c)
+    with pytest.raises(RuntimeError, match="block_size"):
+        ops.forward(torch.zeros(3, 512, device=dev), spec, None, 128, 512, algo="stationary")
+
+
+def test_stationary_full_size_and_linearity(dev):
+    """North-star size (4096^2, b=128, N=8192, fp32): oracle parity on a 256-token slice
+    (the oracle is slow at full size) plus linearity over all 8192 tokens."""
+    rng = np.random.default_rng(0)
+    c = (rng.standard_normal((32, 32, 128)) * 0.01).astype(np.float32)
+    bv = None
+    x = rng.standard_normal((8192, 4096)).astype(np.float32)
+    from bcfft import ops
+    ct = torch.from_numpy(c).to(dev)
+    spec = ops.spectra(ct)
+    xt = torch.from_numpy(x).to(dev)
+    y = ops.forward(xt, spec, bv, 128, 4096, algo="stationary")
+    sl = slice(4000, 4256)
+    ref = O.bc_forward(x[sl], c)
+    e = rel_err(y[sl].cpu().numpy(), ref)
+    assert e < STAT_TOL, e
+    x2 = torch.randn(8192, 4096, device=dev)
+    lhs = ops.forward(2.0 * xt + x2, spec, None, 128, 4096, algo="stationary")
+    rhs = 2.0 * y + ops.forward(x2, spec, None, 128, 4096, algo="stationary")
+    assert ((lhs - rhs).norm() / rhs.norm()).item() < 1e-4

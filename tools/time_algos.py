@@ -1,0 +1,43 @@
+"""Per-algorithm kernel timing of the BC forward at the bench shapes (HIP events on the launch
+stream, mean over iterations). Analysis tool; bench.py is the contract."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "llama-fft_amd"))
+import torch  # noqa: E402
+from bcfft import ops  # noqa: E402
+
+DT = {"fp32": torch.float32, "bf16": torch.bfloat16}
+
+
+def t_one(k, m, b, io, algo, n=8192, iters=50):
+    torch.manual_seed(1)
+    c = (torch.randn(m // b, k // b, b) * 0.01).cuda()
+    spec = ops.spectra(c)
+    x = torch.randn(n, k, device="cuda").to(DT[io])
+    for _ in range(5):
+        ops.forward(x, spec, None, b, m, algo=algo)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        ops.forward(x, spec, None, b, m, algo=algo)
+    e.record()
+    torch.cuda.synchronize()
+    us = s.elapsed_time(e) / iters * 1e3
+    es = 4 if io == "fp32" else 2
+    nbytes = n * k * es + n * m * es + (m // b) * (k // b) * (b // 2 + 1) * 8
+    print(f"{algo:10s} {k}x{m} b{b} {io}: {us:8.1f} us  {nbytes / us / 1e3:7.1f} GB/s  "
+          f"{nbytes / us / 1e3 / 8000:.3f} of 8 TB/s", flush=True)
+
+
+if __name__ == "__main__":
+    shapes = [(4096, 4096, 128, "fp32"), (4096, 4096, 128, "bf16"), (4096, 11008, 128, "bf16"),
+              (4096, 4096, 64, "fp32")]
+    for sh in shapes:
+        for algo in sys.argv[1:] or ["stationary", "mfma", "valu"]:
+            try:
+                t_one(*sh, algo)
+            except RuntimeError as ex:
+                print(algo, sh, "n/a:", str(ex)[:80])
