@@ -45,6 +45,20 @@ def algo_bytes(n, k, m, b, io, bias):
     return n * k * SZ[io] + n * m * SZ[io] + n_out * n_in * (b // 2 + 1) * 8 + (m * SZ[io] if bias else 0)
 
 
+def resolved_kernel(algo, k, b):
+    """(algorithm, kernel symbol, MAC arithmetic) that BCFFT_ALGO=algo runs for this geometry;
+    mirrors bcfft_forward_algo's AUTO rule (csrc/bcfft_kernels.hip)."""
+    n_in = k // b
+    stat_ok = (b == 128 and n_in == 32) or (b == 64 and n_in in (32, 64))
+    if algo == "stationary" or (algo == "auto" and stat_ok):
+        return ("stationary", "bc_forward_stat_kernel",
+                "MFMA fp16: conj(C)*s_C (VGPR-resident) x per-token-scaled X split hi+lo, f32 accumulate")
+    if algo == "mfma" or (algo == "auto" and b <= 128):
+        return ("mfma", "bc_forward_mfma_kernel",
+                "MFMA bf16 hi/lo split (Xhi+Xlo)(Chi+Clo), f32 accumulate")
+    return ("valu", "bc_forward_valu_kernel", "VALU fp32 FMA")
+
+
 def algo_flops(n, k, m, b):
     import math
     n_out, n_in = m // b, k // b
@@ -192,7 +206,8 @@ def main():
 
     variants = []
     if args.variants and rank == 0 and world == 1:
-        for (vk, vm, vb, vio, vn, va) in [(4096, 4096, 128, "fp32", 8192, "valu"),
+        for (vk, vm, vb, vio, vn, va) in [(4096, 4096, 128, "fp32", 8192, "mfma"),
+                                          (4096, 4096, 128, "fp32", 8192, "valu"),
                                           (4096, 4096, 128, "bf16", 8192, "auto"),
                                           (4096, 11008, 128, "bf16", 8192, "auto"),
                                           (11008, 4096, 128, "bf16", 8192, "auto"),
@@ -212,6 +227,7 @@ def main():
             del vl, vx
 
     tag = f"{k}x{m}_b{b}_n{n}_{io}"
+    kname = resolved_kernel(algo, k, b)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_budget > 0:
         cpu = cpu_baseline(k, m, b, io, bool(args.bias), args.cpu_budget)
@@ -235,12 +251,11 @@ def main():
                        "in_features": k, "out_features": m, "block_size": b,
                        "tokens_per_rank": n, "global_tokens": n * world, "io_dtype": io,
                        "bias": bool(args.bias), "parallelism": f"token-shard x{world}",
-                       "algo": algo, "mac": "MFMA bf16 hi/lo split (Xhi+Xlo)(Chi+Clo), f32 accumulate"
-                       if (algo in ("auto", "mfma") and b <= 128) else "VALU fp32 FMA"},
+                       "algo": algo, "algo_resolved": kname[0], "mac": kname[2]},
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                          "traffic": load_traffic(tag),
-                         "kernel": "bc_forward_kernel", "kernel_ms": round(kern, 5),
+                         "kernel": kname[1], "kernel_ms": round(kern, 5),
                          "algorithmic_bytes_per_launch": nbytes,
                          "fp32_tflops": round(algo_flops(n, k, m, b) / (kern * 1e-3) / 1e12, 2),
                          "fp32_valu_peak_tflops": FP32_VALU_TFLOPS},

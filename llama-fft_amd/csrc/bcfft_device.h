@@ -12,11 +12,11 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 // ------------------------------------------------------------------ scalar conversions
 __device__ __forceinline__ float bf16_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
+// hardware round-to-nearest-even (v_cvt_pk_bf16_f32; NaN stays a quiet NaN, denormals kept),
+// the rounding of torch's float -> bfloat16. A software RNE with its NaN test compiled to an
+// exec-masked branch per value here.
 __device__ __forceinline__ uint32_t f32_to_bf16(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;  // keep NaN a (quiet) NaN
-  u += 0x7fffu + ((u >> 16) & 1u);                                 // round to nearest even
-  return u >> 16;
+  return __builtin_bit_cast(uint16_t, (__bf16)f);
 }
 __device__ __forceinline__ float f16_to_f32(uint32_t h) {
   _Float16 v;
@@ -30,6 +30,30 @@ __device__ __forceinline__ uint32_t f32_to_f16(float f) {
   __builtin_memcpy(&s, &v, 2);
   return s;
 }
+// two values -> packed 16-bit pair (low = a), one conversion instruction for bf16
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+typedef __attribute__((ext_vector_type(2))) _Float16 h16x2;
+template <int DT>
+__device__ __forceinline__ uint32_t pack16(float a, float b) {
+  if constexpr (DT == BCFFT_BF16) {
+    const bf16x2 h = {(__bf16)a, (__bf16)b};
+    return __builtin_bit_cast(uint32_t, h);
+  } else {
+    const h16x2 h = {(_Float16)a, (_Float16)b};
+    return __builtin_bit_cast(uint32_t, h);
+  }
+}
+// round a pair to DT and back: the packed pair's halves widened (exact)
+template <int DT>
+__device__ __forceinline__ float2 round_pair(float a, float b) {
+  if constexpr (DT == BCFFT_F32) {
+    return make_float2(a, b);
+  } else {
+    const uint32_t p = pack16<DT>(a, b);
+    if constexpr (DT == BCFFT_BF16) return make_float2(__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u));
+    else return make_float2(f16_to_f32(p & 0xffffu), f16_to_f32(p >> 16));
+  }
+}
 // value-exact emulation of tensor.to(dtype) read back as fp32
 __device__ __forceinline__ float round_to(float v, int dt) {
   if (dt == BCFFT_BF16) return bf16_to_f32(f32_to_bf16(v));
@@ -41,10 +65,8 @@ __device__ __forceinline__ float load_scalar(const void* p, int64_t i, int dt) {
   uint32_t h = ((const uint16_t*)p)[i];
   return dt == BCFFT_BF16 ? bf16_to_f32(h) : f16_to_f32(h);
 }
-// v = hi + lo with hi, lo bf16: returns packed (lo16 = first, hi16 = second) pairs. Internal
-// MFMA operands only, so the hardware RNE conversion (v_cvt_pk_bf16_f32, one instruction per
-// pair) is used; outputs keep the bit-exact software rounding above.
-typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+// v = hi + lo with hi, lo bf16 (hardware RNE, one v_cvt_pk_bf16_f32 per pair): returns packed
+// (lo16 = first, hi16 = second) pairs
 __device__ __forceinline__ void split_bf16(float2 v, uint32_t& hi, uint32_t& lo) {
   const bf16x2 h = {(__bf16)v.x, (__bf16)v.y};
   hi = __builtin_bit_cast(uint32_t, h);
@@ -76,8 +98,8 @@ __device__ __forceinline__ void wait_vmcnt() {
 // workgroup rendezvous on LDS: own LDS traffic complete, then s_barrier; VMEM stays in flight
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-#ifdef BCFFT_ABLATE
-// analysis build only (make ablate): phase switches set through bcfft_set_ablation(), and a
+#if defined(BCFFT_ABLATE) || defined(BCFFT_STAMPS)
+// analysis builds only (make ablate / make stamps): phase switches set through bcfft_set_ablation(), and a
 // per-wave phase timeline (s_memtime at STAMP points) when bcfft_set_stamps() gave a buffer
 // (static: each translation unit has its own copy and its own setter). ANALYSIS_INIT reads both
 // ONCE per kernel into scalars: a per-use read would be a global load + s_waitcnt vmcnt(0) that
@@ -88,7 +110,11 @@ static __device__ unsigned long long* g_stamps;
   const int ablate_flags_ = __builtin_amdgcn_readfirstlane(g_ablate);                          \
   unsigned long long* const stamps_ = g_stamps;                                                \
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory")
+#ifdef BCFFT_ABLATE
 #define ABLATE(bit) (ablate_flags_ & (bit))
+#else                                  // stamps-only build: the product's control flow, timed
+#define ABLATE(bit) 0
+#endif
 #define STAMP_SLOTS 64
 #define STAMP(id)                                                                              \
   do {                                                                                         \

@@ -688,8 +688,8 @@ int bcfft_forward(const void* x, int x_dtype, int64_t n_tokens, int in_features,
                             bias, bias_dtype, y, y_dtype, BCFFT_ALGO_AUTO, stream);
 }
 
-#ifdef BCFFT_ABLATE
-// analysis build only: phase switches of the MFMA kernel (results are WRONG when set):
+#if defined(BCFFT_ABLATE) || defined(BCFFT_STAMPS)
+// analysis builds only: phase switches of the MFMA kernel (results are WRONG when set):
 // 1 skip MFMAs, 2 skip B-fragment loads, 4 skip forward FFT math, 8 skip inverse FFT math,
 // 16 skip x DMA
 int bcfft_set_ablation(int flags) {

@@ -143,16 +143,6 @@ __host__ __device__ inline void stat_sigma(int j, double sg[2]) {
   if (L == 4 && j == 3) { sg[0] = 0; sg[1] = -1; }
 }
 
-// output staging swizzle: 16-B piece p of a y row (lane position with bins k1 holds pieces
-// [k1 NQL, (k1+1) NQL)) -> unit p ^ f(k1) ^ par, conflict-free for the ds_write_b128 of a lane
-// group and the ds_read_b128 that re-reads rows in global order for 1-KiB stores
-template <int L, int NQL>
-__device__ __forceinline__ int y_unit(int p, int gi) {
-  const int k1 = p / NQL;
-  const int f = NQL == 8 ? (L == 4 ? ((k1 & 1) << 2 | (k1 & 2)) : 4 * k1) : (L == 4 ? 2 * (k1 >> 1) : 2 * k1);
-  return p ^ f ^ (gi & (L == 4 ? 1 : 3));
-}
-
 #ifdef BCFFT_MARKS
 #define MARK(n) asm volatile(";MARK " #n)
 #else
@@ -283,45 +273,58 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
   };
 
   // Y image, bin-pair-major: the 16-B unit of bins (2p, 2p+1) of row R = t*NOG + o sits at
-  // p*PS + 16 * (R ^ (p & 15)). PS = 2 A-image bins, so the pairs of wave w's bins cover exactly
-  // the A-image bytes of those bins: each wave overwrites only what it alone has read.
+  // p*PS + 16 * (R ^ (p & SWM)). PS = 2 A-image bins, so the pairs of wave w's bins cover exactly
+  // the A-image bytes of those bins: each wave overwrites only what it alone has read. The
+  // swizzle takes only p's lowest bit (b = 128), which is lane-constant in the inverse's reads of
+  // Y[k] and Y[H-k], so those are one base address per lane plus immediate offsets.
+  // Row map, staging map and the bank-conflict proof of every access: tools/lds_banks.py.
   constexpr int PS = 2 * 32 * NI;
-  auto yunit = [](int p, int R) { return p * PS + 16 * (R ^ (p & 15)); };
-  // inverse rows: group grp -> (t, o); a half-wave's 8 rows differ in bits 1-3 of R
-  auto inv_row = [](int gr, int& t, int& o) {
-    const int w = gr >> 4, h = (gr >> 3) & 1, r8 = gr & 7;
-    t = w >> 1;
-    o = 16 * (w & 1) + 2 * r8 + h;
+  constexpr int SWM = L / 2 - 1;
+  constexpr int RPWI = 64 / L;                      // inverse rows per wave (contiguous block)
+  auto yunit = [](int p, int R) { return p * PS + 16 * (R ^ (p & SWM)); };
+  // inverse group gr -> row R. L = 4: half-wave -> bit 0, group bits (0, 1, 2) -> (2, 1, 3);
+  // L = 2: identity
+  auto inv_row = [](int gr) {
+    if constexpr (L == 4)
+      return (gr & ~15) | ((gr & 1) << 2) | (gr & 2) | ((gr & 4) << 1) | ((gr >> 3) & 1);
+    else
+      return gr;
   };
-  // y staging: piece pc (16 B) of row R -> bin-pair unit spc(pc) of that row (conflict-free
-  // ds_write_b128 from the lane groups and ds_read_b128 in global order for fp32 b = 128)
+  // y staging: 16-B piece pc of output row rho is kept in unit pc of row rho ^ hmap(pc), a row of
+  // the same wave (hmap < RPWI), so the staged pieces of one store instruction spread over the
+  // banks; hmap is linear in the bits of pc
   constexpr int NQL = 32 * ESY / 16;                // 16-B pieces of y per lane
   constexpr int NPR = B * ESY / 16;                 // 16-B pieces per y row
   constexpr int RPI = 64 / NPR;                     // rows per store instruction
-  auto spc = [](int pc) {
-    if constexpr (NQL == 8 && L == 4) {
-      const int k1 = pc >> 3, q = pc & 7;
-      return (k1 & 1) | ((q & 1) << 1) | ((k1 >> 1) << 2) | ((q >> 1) << 3);
-    } else {
-      return pc;
-    }
+  auto hmap = [](int pc) {
+    constexpr int C128F[5] = {5, 8, 0, 1, 2}, C128H[5] = {0, 2, 5, 10, 0};
+    constexpr int C64F[5] = {1, 2, 4, 12, 0}, C64H[5] = {1, 4, 12, 0, 0};
+    const int* c = B == 128 ? (ESY == 4 ? C128F : C128H) : (ESY == 4 ? C64F : C64H);
+    int r = 0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+      if ((pc >> i) & 1) r ^= c[i];
+    return r;
   };
-  // the wave stores the rows it staged (P4 of tile mt), RPI whole rows per 1-KiB instruction
+  // the wave stores the rows it staged (the inverse of tile mt) in global order, RPI whole rows
+  // (1 KiB) per instruction: rows rho0 + q RPI, rho0 = wave RPWI + lane / NPR
   auto store_tile = [&](int64_t mt, const char* regn) {
-    if (wave * 64 / L >= INV_ROWS) return;
+    if (wave * RPWI >= INV_ROWS) return;
     const int64_t stok0 = mt * TT;
     const int64_t ntok = n_tokens - stok0 < TT ? n_tokens - stok0 : TT;
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
         (char*)yv + stok0 * M * ESY, 0, (int)(ntok * M * ESY), 0x00020000);
     const int slane = opaque(lane);
+    const int pc = slane & (NPR - 1);
+    const int rho0 = wave * RPWI + (int)((unsigned)slane / NPR);
+    const int src0 = yunit(pc, rho0 ^ hmap(pc));    // row rho0 + q RPI = rho0 ^ q RPI
+    const int o0 = rho0 & (G::NOG - 1);
+    const int yoff0 = (int)((((int64_t)(rho0 >> 5) * M) + (int64_t)(grp_o * G::NOG + o0) * B) * ESY) + 16 * pc;
+    const int nvalid = n_out - grp_o * G::NOG;      // output blocks of this group that exist
 #pragma unroll
     for (int q = 0; q < NST; ++q) {
-      const int gi = q * RPI + slane / NPR, pc = slane % NPR;
-      int st_t, st_o;
-      inv_row(wave * (64 / L) + gi, st_t, st_o);
-      const int sog = grp_o * G::NOG + st_o;
-      const uint4 d = *reinterpret_cast<const uint4*>(regn + yunit(spc(pc), st_t * G::NOG + st_o));
-      const int yoff = sog < n_out ? (int)(((int64_t)st_t * M + (int64_t)sog * B) * ESY + 16 * pc) : 0x7fff0000;
+      const uint4 d = *reinterpret_cast<const uint4*>(regn + (src0 ^ (16 * q * RPI)));
+      const int yoff = nvalid >= G::NOG || o0 + q * RPI < nvalid ? yoff0 + q * RPI * B * ESY : 0x7fff0000;
       if (!ABLATE(2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d), yrs, yoff, 0, 0);
     }
   };
@@ -343,6 +346,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     const int sb = 1 + 7 * (it & 7);
     STAMP(sb);
     wait_vmcnt<0>();                                // this wave's x rows (its youngest VMEM ops)
+    MARK(fwd_read);
     STAMP(sb + 1);
 
     // ---- forward: x rows -> X' (untangled, packed) in registers; token max |X'| -> slot
@@ -352,7 +356,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     float2 xs[16];
     if (fwd_active) {
       const int ptid = opaque(tid);
-      const int grp = ptid / L, g = ptid % L;
+      const int grp = (int)((unsigned)ptid / L), g = ptid & (L - 1);
       const int frow = grp < FWD_ROWS ? grp : 0;
       const int ft = frow / NI;
       const char* rowp = region + frow * RB;
@@ -373,6 +377,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
 #pragma unroll
       for (int k2 = 1; k2 < 16; ++k2) tw[k2] = twf[g * G::TS + k2];
       float4 uc[16];
+      MARK(fwd_dft);
       if (!ABLATE(4)) {
         dft<16, false>(v);
 #pragma unroll
@@ -381,7 +386,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
 #pragma unroll
       for (int k2 = 0; k2 < 8; ++k2) uc[k2] = uco[g * G::TS + k2];   // in flight under lane_dft
       __builtin_amdgcn_sched_barrier(0);
+      MARK(fwd_lane);
       if (!ABLATE(4)) lane_dft<L, false>(v, g);
+      MARK(untangle);
       // untangle X'[k] = alpha s + beta conj(p), partner bin H - k by DPP
       float mx = 0.f;
 #pragma unroll
@@ -413,7 +420,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     if (tid < 4) slots[((it + 1) & 1) * 4 + tid] = 0u;   // next tile's maxima
     if (fwd_active) {
       const int ptid = opaque(tid);
-      const int grp = ptid / L, g = ptid % L;
+      const int grp = (int)((unsigned)ptid / L), g = ptid & (L - 1);
       const int k1 = k1_of<L>(g);
       const int frow = grp < FWD_ROWS ? grp : 0;
       const int ft = frow / NI, fi = frow % NI;
@@ -438,6 +445,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
         }
       }
     }
+    MARK(store);
     if (it > 0) store_tile(m - gstride, other);     // tile m-1's y, staged in R'
     lds_barrier();                                  // B2: A image complete; R' staging read
     STAMP(sb + 3);
@@ -463,6 +471,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
           araw[fb][ks] = ABLATE(32) ? make_uint4(a_j, kb, f, ks)
                                     : *reinterpret_cast<const uint4*>(aimg + f * (32 * NI) + a_j * (4 * NI) + 16 * ((4 * ks + kb) ^ a_j ^ hf));
       }
+      MARK(mfma);
       float2 ybuf[BW][NT];
 #pragma unroll
       for (int fb = 0; fb < BW; ++fb) {
@@ -496,6 +505,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
           ybuf[fb][nt] = make_float2(acc[nt][0] + acc[nt][1], acc[nt][2] + acc[nt][3]);
       }
       // own A bins were all read (wave-local DS order): Y pairs go over them, 16 B per lane
+      MARK(ywrite);
       wave_lds_sync();
       const int yt = mlane >> 4;
 #pragma unroll
@@ -513,38 +523,43 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     lds_barrier();                                  // B4: Y image complete
     STAMP(sb + 5);
 
+    MARK(inv_read);
     // ---- inverse transforms -> y rows staged in this tile's region (stored next tile)
     if (inv_active) {
       const int ptid = opaque(tid);
-      const int grp = ptid / L, g = ptid % L;
+      const int grp = (int)((unsigned)ptid / L), g = ptid & (L - 1);
       const int k1 = k1_of<L>(g);
-      int inv_t, inv_o;
-      inv_row(grp, inv_t, inv_o);
-      const int R = inv_t * G::NOG + inv_o;
+      const int R = inv_row(grp);
+      const int inv_t = R >> 5, inv_o = R & (G::NOG - 1);
+      // Y[k], k = g + L n2: unit (g >> 1) + (L/2) n2, half g & 1. Y[H-k] = (H-L-L n2) + (L-g):
+      // unit (H-L)/2 - (L/2) n2 + ((L-g) >> 1), half (L-g) & 1 (k = 0 reads past the image,
+      // unused: bin 0 is packed). Swizzle bit p & SWM is lane-constant in both.
+      const int gl = L - g;
+      const char* ykb = region + yunit(g >> 1, R) + 8 * (g & 1);
+      const char* yhb = region + yunit(gl >> 1, R) + 8 * (gl & 1);
       float2 yk[16], yh[16], wk[16];
 #pragma unroll
       for (int hb = 0; hb < 2; ++hb) {
 #pragma unroll
       for (int n2 = 8 * hb; n2 < 8 * hb + 8; ++n2) {
-        const int k = g + L * n2, kh = (H - k) & (H - 1);
-        yk[n2] = *reinterpret_cast<const float2*>(region + yunit(k >> 1, R) + 8 * (k & 1));
-        yh[n2] = *reinterpret_cast<const float2*>(region + yunit(kh >> 1, R) + 8 * (kh & 1));
-        wk[n2] = twb[k];
+        yk[n2] = *reinterpret_cast<const float2*>(ykb + n2 * (L / 2) * PS);
+        yh[n2] = *reinterpret_cast<const float2*>(yhb + ((H - L) / 2 - (L / 2) * n2) * PS);
+        wk[n2] = twb[g + L * n2];
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int n2 = 8 * hb; n2 < 8 * hb + 8; ++n2) {
-        const int k = g + L * n2;
         const float er = yk[n2].x + yh[n2].x, ei = yk[n2].y - yh[n2].y;   // E = Y[k] + conj(Y[H-k])
         const float dr = yk[n2].x - yh[n2].x, di = yk[n2].y + yh[n2].y;   // D = Y[k] - conj(Y[H-k])
         const float2 w = wk[n2];                                          // Zi = E + i D conj(W^k)
         float2 z;
         z.x = er - (di * w.x - dr * w.y);
         z.y = ei + (dr * w.x + di * w.y);
-        if (k == 0) z = make_float2(yk[n2].x + yk[n2].y, yk[n2].x - yk[n2].y);   // packed bin 0
+        if (n2 == 0 && g == 0) z = make_float2(yk[0].x + yk[0].y, yk[0].x - yk[0].y);   // packed bin 0
         v[n2] = z;
       }
       }
+      MARK(inv_dft);
       float2 tw[16];
 #pragma unroll
       for (int k2 = 1; k2 < 16; ++k2) tw[k2] = twi[g * G::TS + k2];
@@ -554,6 +569,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
         for (int k2 = 1; k2 < 16; ++k2) v[k2] = cmul(v[k2], tw[k2]);
         lane_dft<L, true>(v, g);
       }
+      MARK(inv_out);
       // y[32 k1 + 2 k2 + {0,1}] = D (R0, R1) / (s_t s_C), D = stat_decode<L, true>(g)
       const int e_t = __builtin_amdgcn_frexp_expf(__uint_as_float(slot[inv_t]));
       int nsc = 15 - e_t;
@@ -564,7 +580,11 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
       const float c00 = rot ? 0.f : sd, c01 = rot ? -sc : 0.f;
       const float c10 = rot ? sc : 0.f, c11 = rot ? 0.f : sd;
       const float* brow = bias_l + inv_o * B + 32 * k1;
-      wave_lds_sync();                               // this group's Y reads precede its y writes
+      // piece j of this lane's run (unit k1 NQL + j) goes to row X ^ hmap(j), X = R ^ hmap(k1 NQL)
+      const int sx = R ^ hmap(k1 * NQL);
+      char* stb = region + k1 * NQL * PS;
+      auto stage = [&](int j) { return stb + j * PS + 16 * (sx ^ hmap(j) ^ (j & SWM)); };
+      wave_lds_sync();                               // the wave's Y reads precede its y writes
       // 8 outputs (4 registers) per step: .to(x.dtype) :266, + bias :270-271, .to(y dtype)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -572,29 +592,34 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
           const float2 z = v[4 * q + h];
-          o8[2 * h] = round_to(fmaf(c00, z.x, c01 * z.y), XT);
-          o8[2 * h + 1] = round_to(fmaf(c10, z.x, c11 * z.y), XT);
+          o8[2 * h] = fmaf(c00, z.x, c01 * z.y);
+          o8[2 * h + 1] = fmaf(c10, z.x, c11 * z.y);
         }
-        if (bias_dt != BCFFT_NONE) {
-          const float4 b0 = *reinterpret_cast<const float4*>(brow + 8 * q);
-          const float4 b1 = *reinterpret_cast<const float4*>(brow + 8 * q + 4);
-          o8[0] += b0.x; o8[1] += b0.y; o8[2] += b0.z; o8[3] += b0.w;
-          o8[4] += b1.x; o8[5] += b1.y; o8[6] += b1.z; o8[7] += b1.w;
+        // a 16-bit y without bias is ONE rounding (round_to then the cast is the same value)
+        if (Y32 || bias_dt != BCFFT_NONE) {
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const float2 r = round_pair<XT>(o8[2 * h], o8[2 * h + 1]);
+            o8[2 * h] = r.x;
+            o8[2 * h + 1] = r.y;
+          }
+          if (bias_dt != BCFFT_NONE) {
+            const float4 b0 = *reinterpret_cast<const float4*>(brow + 8 * q);
+            const float4 b1 = *reinterpret_cast<const float4*>(brow + 8 * q + 4);
+            o8[0] += b0.x; o8[1] += b0.y; o8[2] += b0.z; o8[3] += b0.w;
+            o8[4] += b1.x; o8[5] += b1.y; o8[6] += b1.z; o8[7] += b1.w;
+          }
         }
         if constexpr (Y32) {
 #pragma unroll
           for (int hq = 0; hq < 2; ++hq) {
-            const int pc = k1 * NQL + 2 * q + hq;
-            *reinterpret_cast<float4*>(region + yunit(spc(pc), R)) =
+            *reinterpret_cast<float4*>(stage(2 * q + hq)) =
                 make_float4(o8[4 * hq], o8[4 * hq + 1], o8[4 * hq + 2], o8[4 * hq + 3]);
           }
         } else {
-          uint32_t hh[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) hh[e] = XT == BCFFT_BF16 ? f32_to_bf16(o8[e]) : f32_to_f16(o8[e]);
-          const int pc = k1 * NQL + q;
-          *reinterpret_cast<uint4*>(region + yunit(spc(pc), R)) =
-              make_uint4(hh[0] | (hh[1] << 16), hh[2] | (hh[3] << 16), hh[4] | (hh[5] << 16), hh[6] | (hh[7] << 16));
+          *reinterpret_cast<uint4*>(stage(q)) =
+              make_uint4(pack16<XT>(o8[0], o8[1]), pack16<XT>(o8[2], o8[3]), pack16<XT>(o8[4], o8[5]),
+                         pack16<XT>(o8[6], o8[7]));
         }
       }
     }
@@ -743,8 +768,8 @@ void launch_stat_image(int b, int n_out, int n_in, void* spec, hipStream_t s) {
 }
 }  // namespace bcfft
 
-#ifdef BCFFT_ABLATE
-// analysis build only: switches / stamp buffer of bc_forward_stat_kernel (this TU's copies).
+#if defined(BCFFT_ABLATE) || defined(BCFFT_STAMPS)
+// analysis builds only: switches / stamp buffer of bc_forward_stat_kernel (this TU's copies).
 // 1 skip MFMAs, 2 skip y stores, 4 skip forward FFT math, 8 skip inverse FFT math, 16 skip x DMA,
 // 32 skip A-fragment LDS reads, 64 skip the A im-row transform
 extern "C" int bcfft_set_ablation_stat(int flags) {

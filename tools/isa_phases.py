@@ -12,6 +12,9 @@ j = s.index(".Lfunc_end", i)
 lines = [l.strip() for l in s[i:j].split("\n")]
 segs = [[]]
 for l in lines:
+    if l.startswith(";MARK"):                 # -DBCFFT_MARKS phase markers
+        segs.append([l])
+        continue
     if not l or l.startswith(";") or l.startswith(".") or l.endswith(":"):
         continue
     op = l.split()[0]
@@ -39,5 +42,6 @@ def cls(op):
 
 
 for n, seg in enumerate(segs):
-    c = collections.Counter(cls(o) for o in seg)
-    print(f"seg {n:2d}: " + "  ".join(f"{k} {c[k]:4d}" for k in ("valu", "dpp", "mfma", "lds", "vmem", "nop", "wait", "salu")))
+    c = collections.Counter(cls(o) for o in seg if not o.startswith(";"))
+    tag = seg[0] if seg and seg[0].startswith(";MARK") else ""
+    print(f"seg {n:2d} {tag:8s}: " + "  ".join(f"{k} {c[k]:4d}" for k in ("valu", "dpp", "mfma", "lds", "vmem", "nop", "wait", "salu")))

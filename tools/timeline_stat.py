@@ -1,6 +1,7 @@
 """Phase timeline and ablations of the stationary-weight kernel (analysis build only).
 
-Loads lib/libbcfft_ablate.so (`make -C llama-fft_amd ablate`). Every wave stamps s_memtime at
+Loads lib/libbcfft_ablate.so (`make -C llama-fft_amd ablate`), or with TIMELINE_BUILD=stamps
+lib/libbcfft_stamps.so (`make stamps`: stamps only, the product's control flow, no switches). Every wave stamps s_memtime at
 the STAMP points of bc_forward_stat_kernel (bcfft_stat.hip):
   0 start | per M-tile it (base 1 + 7 (it % 8)): +0 loop top, +1 own x rows landed,
   +2 after B1 (forward + untangle + token max), +3 after B2 (split, A image, previous stores),
@@ -15,7 +16,9 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["BCFFT_LIB_PATH"] = os.path.join(ROOT, "llama-fft_amd", "lib", "libbcfft_ablate.so")
+STAMPS_ONLY = os.environ.get("TIMELINE_BUILD", "ablate") == "stamps"   # product control flow
+os.environ["BCFFT_LIB_PATH"] = os.path.join(ROOT, "llama-fft_amd", "lib",
+                                            "libbcfft_stamps.so" if STAMPS_ONLY else "libbcfft_ablate.so")
 sys.path.insert(0, os.path.join(ROOT, "llama-fft_amd"))
 import torch  # noqa: E402
 from bcfft import _lib, ops  # noqa: E402
@@ -70,7 +73,7 @@ def run(k, m, b, io, n):
         return st, seg
 
     print(f"{'flags':14s} {'us':>7s} " + " ".join(f"{h:>11s}" for h in SEG) + "   sum/tile")
-    for name, fl in FLAGS.items():
+    for name, fl in ({"full": 0} if STAMPS_ONLY else FLAGS).items():
         _lib.check(lib.bcfft_set_ablation_stat(fl), "ablation")
         us = timeit()
         _, seg = stamps()
