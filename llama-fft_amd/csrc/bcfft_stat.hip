@@ -8,19 +8,24 @@
 //    workgroup owns one output group of 32 blocks (= 4096 outputs at b = 128). It loads that
 //    group's packed weight spectra ONCE, as fp16 MFMA B fragments scaled by a power of two
 //    s_C: K/32 = 128 VGPRs per lane. Wave w keeps bins [w*BW, (w+1)*BW).
-//  * Tokens go through in M-tiles of 4. x arrives by LDS-DMA into one of two 64 KiB regions,
-//    one M-tile ahead. Each M-tile runs three phases, separated by workgroup barriers:
-//      forward  one row (token, input block) per L = b/32 lanes, 16 complex points per lane:
-//               an in-register 16-point DFT, the four-step twiddle, an L-point DFT across the
-//               lanes (DPP), then the real-FFT untangle (partner bin from DPP). The result is
-//               scaled by a per-token power of two s_t, split into fp16 hi + lo, and written as
-//               the MFMA A image in place over x.
-//      CMAC     per bin: v_mfma_f32_16x16x32_f16 with rows (token, re/im, hi/lo) x 16 output
-//               blocks, K = 16 input blocks x (re, im); B = stationary conj(C) fragments.
-//               The per-bin results go to LDS rows (token, output block).
-//      inverse  the real-FFT pre-process from LDS, a 16-point DFT, twiddle, L-point DFT across
-//               the lanes, scale 1/(s_t s_C), cast/bias/cast, then 16-B buffer stores. Each lane
-//               ends up holding 32 contiguous outputs.
+//  * Tokens go through in M-tiles of 4, two 64 KiB LDS regions alternating, each cut into
+//    8 KiB slots. Slot w is wave w's: its x rows arrive there by LDS-DMA (issued by wave w a
+//    whole tile ahead), its forward replaces them in place by its A fragments, and after the
+//    MFMAs the slot holds the Y units of the inverse rows wave w transforms and stores. Two
+//    workgroup barriers per M-tile:
+//      P1  inverse of the previous tile, its y stores, the next tile's DMA, then the forward:
+//          one row (token, input block) per L = b/32 lanes, 16 complex points per lane: an
+//          in-register 16-point DFT, the four-step twiddle, an L-point DFT across the lanes
+//          (DPP), the real-FFT untangle (partner bin by DPP). The wave's rows are one token's
+//          K-step(s), so the wave's own max |X'| sets a power-of-two scale; X' is split into
+//          fp16 hi + lo A fragments.                                           | barrier |
+//      P2  per bin: v_mfma_f32_16x16x32_f16 with rows (token, re/im, hi/lo) x 16 output
+//          blocks, K = 16 input blocks x (re, im); B = stationary conj(C) fragments. A token's
+//          K-steps are brought to one exponent by exact fp16 power-of-two factors folded into
+//          the im-row transform; the per-bin results go to the Y units.          | barrier |
+//      The inverse: the real-FFT pre-process from LDS, a 16-point DFT, twiddle, L-point DFT
+//      across the lanes, scale 1/(s_t s_C), cast/bias/cast, staged in the slot and stored as
+//      1 KiB buffer stores. Each lane ends up holding 32 contiguous outputs.
 //  * Numerics: X is split into two fp16 terms (~2^-21). C is one fp16 term (~2^-11 relative
 //    per bin, ~3e-4 relative on the layer output). Accumulation is fp32. This is inside the
 //    north star's 1e-3. bc_forward_mfma_kernel (bf16 hi/lo on both operands, ~1e-5) and
@@ -149,6 +154,28 @@ __host__ __device__ inline void stat_sigma(int j, double sg[2]) {
 #define MARK(n) do {} while (0)
 #endif
 
+// packed fp16 product of two fp16 pairs (v_pk_mul_f16)
+__device__ __forceinline__ uint32_t pkmul(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2, a) * __builtin_bit_cast(f16x2, b));
+}
+
+// max over the wave's 64 lanes, uniform: quad and row by DPP, the four rows by readlane
+__device__ __forceinline__ float wave_max(float v) {
+  v = fmaxf(v, dpp<DPP_XOR1>(v));
+  v = fmaxf(v, dpp<DPP_XOR2>(v));
+  v = fmaxf(v, dpp<0x141>(v));                     // row_half_mirror
+  v = fmaxf(v, dpp<0x140>(v));                     // row_mirror
+  const int u = __float_as_int(v);
+  const float a = fmaxf(__int_as_float(__builtin_amdgcn_readlane(u, 0)), __int_as_float(__builtin_amdgcn_readlane(u, 16)));
+  const float b = fmaxf(__int_as_float(__builtin_amdgcn_readlane(u, 32)), __int_as_float(__builtin_amdgcn_readlane(u, 48)));
+  return fmaxf(a, b);
+}
+// scale exponent for fp16 hi/lo: 2^nsc mx < 2^15, clamped so 2^nsc and 2^-nsc stay normal
+__device__ __forceinline__ int stat_scale_exp(float mx) {
+  const int nsc = 15 - __builtin_amdgcn_frexp_expf(mx);
+  return nsc < -126 ? -126 : (nsc > 126 ? 126 : nsc);
+}
+
 // x staging swizzle (16-B units of a row) that keeps the forward DPP-group reads conflict-free
 template <int L, int ES>
 __device__ __forceinline__ int swz_x(int r) {
@@ -248,54 +275,47 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
           creg[fb][ks][nt] = __builtin_bit_cast(f16x8, img[((fb * KS + ks) * NT + nt) * 64]);
   }
 
-  // ---- x M-tile -> region by LDS-DMA. Each wave loads exactly the x rows its own forward
-  // groups transform (RPWF rows = NDMA 1-KiB pieces), so its own vmcnt wait is all it needs
-  // before reading them. The tile's 4 token rows are one contiguous span of x: a lane's source
-  // offset is its LDS byte with the row's unit swizzle (swz_x) XORed in; the buffer range check
-  // zero-fills rows past n_tokens (those tokens are never stored).
-  auto dma_tile = [&](int64_t m, char* region) {
-    if (wave >= FWD_ROWS / RPWF) return;
-    const int64_t tok0 = m * TT;
-    const int64_t ntok = n_tokens - tok0 < TT ? n_tokens - tok0 : TT;
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<char*>((const char*)xv) + tok0 * K * ES, 0, (int)(ntok * K * ES), 0x00020000);
-    const int dlane = opaque(lane);
-#pragma unroll
-    for (int q = 0; q < NDMA; ++q) {
-      const int c = wave * NDMA + q;
-      const int byte = c * 1024 + dlane * 16;
-      const int voff = byte ^ (swz_x<L, ES>(byte / RB) << 4);
-      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(region + c * 1024));
-      uint32_t keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep) : "v"(voff), "s"(xrs), "s"(dst) : "memory");
-    }
-  };
+  // ---- LDS region layout: NWF slots of 8 KiB. Slot s belongs to forward wave s: that wave's
+  // x rows land there (LDS-DMA), its forward replaces them in place by its A fragments (no other
+  // wave reads or writes the slot in that phase), and after the MFMAs slot s holds the Y units of
+  // the inverse rows [s RPWI, (s+1) RPWI), which inverse wave s reads, replaces by its staged y
+  // rows and stores. Bank proofs of every access: tools/lds_banks.py.
+  constexpr int SLOT = 8192;
+  constexpr int NQ = RPWF / 4;                     // block quads per slot
+  constexpr int NWF = FWD_ROWS / RPWF;             // forward waves = A slots
+  constexpr int RPWI = 64 / L;                     // inverse rows per wave
+  constexpr int NWI = INV_ROWS / RPWI;             // inverse waves = Y slots
+  constexpr int SA = L == 4 ? 1 : 2;               // A swizzle shift: log2(8 / L)
+  constexpr int SWM = L / 2 - 1;                   // Y swizzle mask
+  static_assert(RPWF * H * 8 == SLOT && RPWI * (H / 2) * 16 == SLOT, "slot = A rows = Y rows");
+  static_assert(RPWF * RB <= SLOT && NWF * SLOT <= G::REGION && NWI <= NWF, "slots");
+  static_assert(NI % RPWF == 0 || RPWF % NI == 0, "a forward wave's rows are one token");
+  int* wsc = reinterpret_cast<int*>(slots);        // per forward wave: its scale exponent
 
-  // Y image, bin-pair-major: the 16-B unit of bins (2p, 2p+1) of row R = t*NOG + o sits at
-  // p*PS + 16 * (R ^ (p & SWM)). PS = 2 A-image bins, so the pairs of wave w's bins cover exactly
-  // the A-image bytes of those bins: each wave overwrites only what it alone has read. The
-  // swizzle takes only p's lowest bit (b = 128), which is lane-constant in the inverse's reads of
-  // Y[k] and Y[H-k], so those are one base address per lane plus immediate offsets.
-  // Row map, staging map and the bank-conflict proof of every access: tools/lds_banks.py.
-  constexpr int PS = 2 * 32 * NI;
-  constexpr int SWM = L / 2 - 1;
-  constexpr int RPWI = 64 / L;                      // inverse rows per wave (contiguous block)
-  auto yunit = [](int p, int R) { return p * PS + 16 * (R ^ (p & SWM)); };
-  // inverse group gr -> row R. L = 4: half-wave -> bit 0, group bits (0, 1, 2) -> (2, 1, 3);
-  // L = 2: identity
-  auto inv_row = [](int gr) {
-    if constexpr (L == 4)
-      return (gr & ~15) | ((gr & 1) << 2) | (gr & 2) | ((gr & 4) << 1) | ((gr >> 3) & 1);
-    else
-      return gr;
+  // A fragment unit (16 B: 4 blocks x (re, im) fp16 of bin f, precision prec, block quad lq)
+  // within slot s; the XOR keeps the lanes of the forward's writes and of the MFMA reads on
+  // distinct banks and never leaves bin f
+  auto aunit = [](int f, int prec, int lq, int s) {
+    const int tsw = s / (NWF / 2);
+    return 16 * ((f * 2 * NQ + prec * NQ + lq) ^ (((f >> 4) ^ tsw) << SA));
   };
-  // y staging: 16-B piece pc of output row rho is kept in unit pc of row rho ^ hmap(pc), a row of
-  // the same wave (hmap < RPWI), so the staged pieces of one store instruction spread over the
-  // banks; hmap is linear in the bits of pc
-  constexpr int NQL = 32 * ESY / 16;                // 16-B pieces of y per lane
-  constexpr int NPR = B * ESY / 16;                 // 16-B pieces per y row
-  constexpr int RPI = 64 / NPR;                     // rows per store instruction
+  // Y unit (bins 2p, 2p+1) of inverse row r of slot w; the units of bins (2p, 2p+1) of every
+  // row of the slot are exactly the A units of those two bins there (an MFMA wave overwrites
+  // only what it alone has read). The swizzle bit p & SWM is lane-constant in the inverse's reads.
+  auto yunit = [](int p, int r) { return 16 * (p * RPWI + (r ^ (p & SWM))); };
+  // inverse group gi (within its wave) -> row r. L = 4: half-wave -> bit 0, group bits
+  // (0, 1, 2) -> (2, 1, 3); L = 2: identity
+  auto inv_row = [](int gi) {
+    if constexpr (L == 4)
+      return ((gi & 1) << 2) | (gi & 2) | ((gi & 4) << 1) | ((gi >> 3) & 1);
+    else
+      return gi;
+  };
+  // y staging: 16-B piece pc of row r goes to unit pc of row r ^ hmap(pc) (same slot), which
+  // spreads one store instruction's pieces over the banks; hmap is linear in the bits of pc
+  constexpr int NQL = 32 * ESY / 16;               // 16-B pieces of y per lane
+  constexpr int NPR = B * ESY / 16;                // 16-B pieces per y row
+  constexpr int RPI = 64 / NPR;                    // rows per store instruction
   auto hmap = [](int pc) {
     constexpr int C128F[5] = {5, 8, 0, 1, 2}, C128H[5] = {0, 2, 5, 10, 0};
     constexpr int C64F[5] = {1, 2, 4, 12, 0}, C64H[5] = {1, 4, 12, 0, 0};
@@ -306,18 +326,43 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
       if ((pc >> i) & 1) r ^= c[i];
     return r;
   };
-  // the wave stores the rows it staged (the inverse of tile mt) in global order, RPI whole rows
-  // (1 KiB) per instruction: rows rho0 + q RPI, rho0 = wave RPWI + lane / NPR
+
+  // ---- x M-tile -> region by LDS-DMA: forward wave w loads its own RPWF rows (NDMA 1-KiB
+  // pieces) into slot w, so its own vmcnt wait is all it needs before reading them. The tile's
+  // 4 token rows are one contiguous span of x: a lane's source offset is its row byte with the
+  // row's unit swizzle (swz_x) XORed in; the buffer range check zero-fills rows past n_tokens
+  // (those tokens are never stored).
+  auto dma_tile = [&](int64_t m, char* region) {
+    if (wave >= NWF) return;
+    const int64_t tok0 = m * TT;
+    const int64_t ntok = n_tokens - tok0 < TT ? n_tokens - tok0 : TT;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>((const char*)xv) + tok0 * K * ES, 0, (int)(ntok * K * ES), 0x00020000);
+    const int dlane = opaque(lane);
+#pragma unroll
+    for (int q = 0; q < NDMA; ++q) {
+      const int byte = (wave * NDMA + q) * 1024 + dlane * 16;
+      const int voff = byte ^ (swz_x<L, ES>(byte / RB) << 4);
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(region + wave * SLOT + q * 1024));
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(voff), "s"(xrs), "s"(dst) : "memory");
+    }
+  };
+
+  // the inverse wave stores the rows it staged, in global order, RPI whole rows (1 KiB) per
+  // instruction: rows r0 + q RPI of its slot, r0 = lane / NPR
   auto store_tile = [&](int64_t mt, const char* regn) {
-    if (wave * RPWI >= INV_ROWS) return;
+    if (wave >= NWI) return;
     const int64_t stok0 = mt * TT;
     const int64_t ntok = n_tokens - stok0 < TT ? n_tokens - stok0 : TT;
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
         (char*)yv + stok0 * M * ESY, 0, (int)(ntok * M * ESY), 0x00020000);
     const int slane = opaque(lane);
     const int pc = slane & (NPR - 1);
-    const int rho0 = wave * RPWI + (int)((unsigned)slane / NPR);
-    const int src0 = yunit(pc, rho0 ^ hmap(pc));    // row rho0 + q RPI = rho0 ^ q RPI
+    const int r0 = (int)((unsigned)slane / NPR);
+    const int src0 = wave * SLOT + yunit(pc, r0 ^ hmap(pc));   // row r0 + q RPI = r0 ^ q RPI
+    const int rho0 = wave * RPWI + r0;                          // y row: token rho >> 5, block rho & 31
     const int o0 = rho0 & (G::NOG - 1);
     const int yoff0 = (int)((((int64_t)(rho0 >> 5) * M) + (int64_t)(grp_o * G::NOG + o0) * B) * ESY) + 16 * pc;
     const int nvalid = n_out - grp_o * G::NOG;      // output blocks of this group that exist
@@ -329,167 +374,161 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     }
   };
 
-  // Pipeline per tile m (regions R = R[it & 1], R' = the other), three barriers:
-  //   own x rows landed (vmcnt) | forward FFT + untangle, token max -> LDS | B1 | scale, split ->
-  //   A image in place; stores of tile m-1 from R' | B2 | DMA x(m+1) -> R', MFMAs, own Y pairs
-  //   over own A bins | B4 | inverse, y staged into own Y rows (stored during tile m+1)
-  int64_t m = blockIdx.x;
-  STAMP(0);
-  if (m < n_mtiles && !ABLATE(16)) dma_tile(m, lds);
-
-  int it = 0;
-  for (; m < n_mtiles; ++it, m += gstride) {
-    char* region = lds + (it & 1) * G::REGION;
-    char* other = lds + ((it + 1) & 1) * G::REGION;
-    uint32_t* slot = slots + (it & 1) * 4;
-    const bool more = m + gstride < n_mtiles;
-    const int sb = 1 + 7 * (it & 7);
-    STAMP(sb);
-    wait_vmcnt<0>();                                // this wave's x rows (its youngest VMEM ops)
+  // ---- forward of one M-tile (wave w < NWF, slot w): x rows -> real-FFT bins X' -> scaled
+  // fp16 hi/lo A fragments in place. All RPWF rows of the wave are one token's K-step(s): the
+  // wave's own max |X'| sets the scale s = 2^(15 - E) (max < 2^E), exponent posted to wsc[w].
+  auto forward = [&](char* region, int younger) {
+    // this wave's x rows landed: everything but the `younger` VMEM ops issued after them
+    if (younger == NST + NDMA) wait_vmcnt<NST + NDMA>();
+    else if (younger == NST) wait_vmcnt<NST>();
+    else if (younger == NDMA) wait_vmcnt<NDMA>();
+    else wait_vmcnt<0>();
     MARK(fwd_read);
-    STAMP(sb + 1);
-
-    // ---- forward: x rows -> X' (untangled, packed) in registers; token max |X'| -> slot
-    const bool fwd_active = wave * 64 / L < FWD_ROWS;
-    const bool inv_active = wave * 64 / L < INV_ROWS;
+    const int ptid = opaque(tid);
+    const int li = (int)((unsigned)(ptid & 63) / L), g = ptid & (L - 1);
+    const int k1 = k1_of<L>(g);
+    char* slot = region + wave * SLOT;
     float2 v[16];
-    float2 xs[16];
-    if (fwd_active) {
-      const int ptid = opaque(tid);
-      const int grp = (int)((unsigned)ptid / L), g = ptid & (L - 1);
-      const int frow = grp < FWD_ROWS ? grp : 0;
-      const int ft = frow / NI;
-      const char* rowp = region + frow * RB;
+    {
+      const char* rowp = slot + li * RB;
 #pragma unroll
       for (int n2 = 0; n2 < 16; ++n2) {
         const int n = g + L * n2;
         if constexpr (ES == 4) {
           const int off = 8 * n;
-          v[n2] = *reinterpret_cast<const float2*>(rowp + (((off >> 4) ^ swz_x<L, ES>(frow)) << 4) + (off & 15));
+          v[n2] = *reinterpret_cast<const float2*>(rowp + (((off >> 4) ^ swz_x<L, ES>(li)) << 4) + (off & 15));
         } else {
           const int off = 4 * n;
-          const uint32_t w = *reinterpret_cast<const uint32_t*>(rowp + (((off >> 4) ^ swz_x<L, ES>(frow)) << 4) + (off & 15));
+          const uint32_t w = *reinterpret_cast<const uint32_t*>(rowp + (((off >> 4) ^ swz_x<L, ES>(li)) << 4) + (off & 15));
           v[n2] = XT == BCFFT_BF16 ? make_float2(bf16_to_f32(w & 0xffffu), bf16_to_f32(w >> 16))
                                    : make_float2(f16_to_f32(w & 0xffffu), f16_to_f32(w >> 16));
         }
       }
-      float2 tw[16];                                // four-step twiddles, issued ahead of the DFT
-#pragma unroll
-      for (int k2 = 1; k2 < 16; ++k2) tw[k2] = twf[g * G::TS + k2];
-      float4 uc[16];
-      MARK(fwd_dft);
-      if (!ABLATE(4)) {
-        dft<16, false>(v);
-#pragma unroll
-        for (int k2 = 1; k2 < 16; ++k2) v[k2] = cmul(v[k2], tw[k2]);
-      }
-#pragma unroll
-      for (int k2 = 0; k2 < 8; ++k2) uc[k2] = uco[g * G::TS + k2];   // in flight under lane_dft
-      __builtin_amdgcn_sched_barrier(0);
-      MARK(fwd_lane);
-      if (!ABLATE(4)) lane_dft<L, false>(v, g);
-      MARK(untangle);
-      // untangle X'[k] = alpha s + beta conj(p), partner bin H - k by DPP
-      float mx = 0.f;
-#pragma unroll
-      for (int k2 = 0; k2 < 16; ++k2) {
-        if (k2 == 4) {                              // second half of the coefficients
-#pragma unroll
-          for (int kk = 8; kk < 16; ++kk) uc[kk] = uco[g * G::TS + kk];
-        }
-        const int src = k2 == 0 ? 0 : 16 - k2;
-        float px, py;
-        if constexpr (L == 4) {
-          if (k2 == 0) { px = dpp<DPP_P0>(v[0].x); py = dpp<DPP_P0>(v[0].y); }
-          else { px = dpp<DPP_XOR3>(v[src].x); py = dpp<DPP_XOR3>(v[src].y); }
-        } else {
-          if (k2 == 0) { px = v[0].x; py = v[0].y; }
-          else { px = dpp<DPP_XOR1>(v[src].x); py = dpp<DPP_XOR1>(v[src].y); }
-        }
-        const float4 c = uc[k2];
-        xs[k2].x = fmaf(c.x, v[k2].x, fmaf(-c.y, v[k2].y, fmaf(c.z, px, c.w * py)));
-        xs[k2].y = fmaf(c.x, v[k2].y, fmaf(c.y, v[k2].x, fmaf(c.w, px, -c.z * py)));
-        mx = fmaxf(mx, fmaxf(fabsf(xs[k2].x), fabsf(xs[k2].y)));
-      }
-      mx = fmaxf(mx, dpp<DPP_XOR1>(mx));
-      if constexpr (L == 4) mx = fmaxf(mx, dpp<DPP_XOR2>(mx));
-      if (g == 0 && grp < FWD_ROWS) atomicMax(&slot[ft], __float_as_uint(mx));
     }
-    lds_barrier();                                  // B1: every x row read, token maxima posted
-    STAMP(sb + 2);
-    if (tid < 4) slots[((it + 1) & 1) * 4 + tid] = 0u;   // next tile's maxima
-    if (fwd_active) {
-      const int ptid = opaque(tid);
-      const int grp = (int)((unsigned)ptid / L), g = ptid & (L - 1);
-      const int k1 = k1_of<L>(g);
-      const int frow = grp < FWD_ROWS ? grp : 0;
-      const int ft = frow / NI, fi = frow % NI;
-      // s_t = 2^(15 - E), max |X'| < 2^E over the token: X' s_t fits fp16 with headroom
-      const int e_t = __builtin_amdgcn_frexp_expf(__uint_as_float(slot[ft]));
-      int nsc = 15 - e_t;
-      nsc = nsc < -126 ? -126 : (nsc > 127 ? 127 : nsc);
-      const float s_t = __int_as_float((nsc + 127) << 23);
-      char* aimg = region;
-      const int hf = k1 * (8 / L);
+    float2 tw[16];                                  // four-step twiddles, issued ahead of the DFT
 #pragma unroll
-      for (int k2 = 0; k2 < 16; ++k2) {
-        const float ox = xs[k2].x * s_t, oy = xs[k2].y * s_t;
-        const f16x2 hi = __builtin_bit_cast(f16x2, __builtin_amdgcn_cvt_pkrtz(ox, oy));
-        const f16x2 lo = __builtin_bit_cast(f16x2, __builtin_amdgcn_cvt_pkrtz(ox - (float)hi.x, oy - (float)hi.y));
-        const int f = k2 + 16 * k1;
-        if (grp < FWD_ROWS) {
-          char* base = aimg + f * (32 * NI);
-          const int j0 = 2 * ft, j1 = 2 * ft + 1;
-          *reinterpret_cast<f16x2*>(base + j0 * (4 * NI) + 16 * (((fi >> 2) ^ j0 ^ hf)) + 4 * (fi & 3)) = hi;
-          *reinterpret_cast<f16x2*>(base + j1 * (4 * NI) + 16 * (((fi >> 2) ^ j1 ^ hf)) + 4 * (fi & 3)) = lo;
-        }
-      }
+    for (int k2 = 1; k2 < 16; ++k2) tw[k2] = twf[g * G::TS + k2];
+    float4 uc[16];
+    MARK(fwd_dft);
+    if (!ABLATE(4)) {
+      dft<16, false>(v);
+#pragma unroll
+      for (int k2 = 1; k2 < 16; ++k2) v[k2] = cmul(v[k2], tw[k2]);
     }
-    MARK(store);
-    if (it > 0) store_tile(m - gstride, other);     // tile m-1's y, staged in R'
-    lds_barrier();                                  // B2: A image complete; R' staging read
-    STAMP(sb + 3);
-    if (more && !ABLATE(16)) dma_tile(m + gstride, other);
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) uc[k2] = uco[g * G::TS + k2];   // in flight under lane_dft
+    __builtin_amdgcn_sched_barrier(0);
+    MARK(fwd_lane);
+    if (!ABLATE(4)) lane_dft<L, false>(v, g);
+    MARK(untangle);
+    // untangle X'[k] = alpha s + beta conj(p), partner bin H - k by DPP
+    float2 xs[16];
+    float mx = 0.f;
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) {
+      if (k2 == 4) {                                // second half of the coefficients
+#pragma unroll
+        for (int kk = 8; kk < 16; ++kk) uc[kk] = uco[g * G::TS + kk];
+      }
+      const int src = k2 == 0 ? 0 : 16 - k2;
+      float px, py;
+      if constexpr (L == 4) {
+        if (k2 == 0) { px = dpp<DPP_P0>(v[0].x); py = dpp<DPP_P0>(v[0].y); }
+        else { px = dpp<DPP_XOR3>(v[src].x); py = dpp<DPP_XOR3>(v[src].y); }
+      } else {
+        if (k2 == 0) { px = v[0].x; py = v[0].y; }
+        else { px = dpp<DPP_XOR1>(v[src].x); py = dpp<DPP_XOR1>(v[src].y); }
+      }
+      const float4 c = uc[k2];
+      xs[k2].x = fmaf(c.x, v[k2].x, fmaf(-c.y, v[k2].y, fmaf(c.z, px, c.w * py)));
+      xs[k2].y = fmaf(c.x, v[k2].y, fmaf(c.y, v[k2].x, fmaf(c.w, px, -c.z * py)));
+      mx = fmaxf(mx, fmaxf(fabsf(xs[k2].x), fabsf(xs[k2].y)));
+    }
+    // wave max -> scale exponent nsc: 2^nsc max|X'| < 2^15 (fp16 hi with headroom)
+    const int nsc = stat_scale_exp(wave_max(mx));
+    if (lane == 0) wsc[wave] = nsc;
+    const float s_w = __int_as_float((nsc + 127) << 23);
+    MARK(split);
+    // hi = fp16(X' s) (round toward zero), lo = fp16(X' s - hi): two fp16 terms ~2^-21
+    char* abase = slot + 4 * (li & 3);
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) {
+      const float ox = xs[k2].x * s_w, oy = xs[k2].y * s_w;
+      const f16x2 hi = __builtin_bit_cast(f16x2, __builtin_amdgcn_cvt_pkrtz(ox, oy));
+      const f16x2 lo = __builtin_bit_cast(f16x2, __builtin_amdgcn_cvt_pkrtz(ox - (float)hi.x, oy - (float)hi.y));
+      const int f = k2 + 16 * k1;
+      *reinterpret_cast<f16x2*>(abase + aunit(f, 0, li >> 2, wave)) = hi;
+      *reinterpret_cast<f16x2*>(abase + aunit(f, 1, li >> 2, wave)) = lo;
+    }
+  };
 
-    // ---- per-bin complex MAC on the matrix cores; results overwrite this wave's own A bins
-    {
-      const int mlane = opaque(lane);
-      const int arow = mlane & 15, kb = mlane >> 4;  // A row (token, re/im, hi/lo), K quad
-      const int a_t = arow >> 2, a_reim = (arow >> 1) & 1, a_prec = arow & 1;
-      const int a_j = 2 * a_t + a_prec;
-      const uint32_t a_sel = a_reim ? 0x01000302u : 0x03020100u;   // im rows: (re, im) -> (im, -re)
-      const uint32_t a_xor = a_reim ? 0x80000000u : 0u;
-      const uint32_t a_bin0 = a_reim ? 0xffff0000u : 0x0000ffffu;  // bin 0: (X0, 0) / (0, X_H)
-      char* aimg = region;
-      uint4 araw[BW][KS];                           // every A fragment of the wave's bins, read
-#pragma unroll                                       // before the first MFMA
-      for (int fb = 0; fb < BW; ++fb) {
-        const int f = wave * BW + fb;
-        const int hf = (f >> 4) * (8 / L);
+  // ---- per-bin complex MAC on the matrix cores (all waves): wave w's bins f = w BW + fb; the
+  // Y pairs overwrite this wave's own A bins.
+  auto cmac = [&](char* region) {
+    const int mlane = opaque(lane);
+    const int arow = mlane & 15, kb = mlane >> 4;   // A row (token, re/im, hi/lo), K quad
+    const int a_t = arow >> 2, a_reim = (arow >> 1) & 1, a_prec = arow & 1;
+    const uint32_t a_sel = a_reim ? 0x01000302u : 0x03020100u;   // im rows: (re, im) -> (im, re)
+    const int yt = mlane >> 4;                      // accumulator rows 4 yt + {re hi, re lo, im hi, im lo}
+    // Each K-step was formed at its forward wave's own scale 2^nsc. A token's K-steps are brought
+    // to its smallest exponent by an exact power-of-two factor folded into the packed fp16
+    // multiply that also applies the im-row sign: (f, f) on re rows, (f, -f) on im rows (after the
+    // swap), (f, 0) / (0, f) on bin 0's rows. Same numerics as one scale per token.
+    int nmin = 127, nminy = 127;
+    int nk[KS];
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
-          araw[fb][ks] = ABLATE(32) ? make_uint4(a_j, kb, f, ks)
-                                    : *reinterpret_cast<const uint4*>(aimg + f * (32 * NI) + a_j * (4 * NI) + 16 * ((4 * ks + kb) ^ a_j ^ hf));
+    for (int ks = 0; ks < KS; ++ks) {
+      nk[ks] = wsc[(a_t * NI + 16 * ks) / RPWF];
+      nmin = min(nmin, nk[ks]);
+      nminy = min(nminy, wsc[(yt * NI + 16 * ks) / RPWF]);
+    }
+    uint32_t amul[KS], amul0[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int d = nk[ks] - nmin;                  // factor 2^-d as fp16 (subnormal / 0 far down)
+      const uint32_t h = d <= 14 ? (uint32_t)(15 - d) << 10 : (d <= 24 ? 1u << (24 - d) : 0u);
+      amul[ks] = a_reim ? (h | ((h | 0x8000u) << 16)) : (h | (h << 16));
+      amul0[ks] = a_reim ? (h << 16) : h;
+    }
+    const float ry = __int_as_float((127 - nminy) << 23);   // 2^-nsc of the accumulator's token
+    uint4 araw[BW][KS];                             // every A fragment of the wave's bins, issued
+#pragma unroll                                       // up front in bin order (counted waits)
+    for (int fb = 0; fb < BW; ++fb) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int row0 = a_t * NI + 16 * ks;
+        const int s = row0 / RPWF, lq = (row0 % RPWF) / 4 + kb;
+        const int f = wave * BW + fb;
+        araw[fb][ks] = ABLATE(32) ? make_uint4(a_t, kb, f, ks)
+                                  : *reinterpret_cast<const uint4*>(region + s * SLOT + aunit(f, a_prec, lq, s));
       }
-      MARK(mfma);
-      float2 ybuf[BW][NT];
+    }
+    // a bin pair's Y goes over the wave's own A units of those bins once its MFMAs are done: the
+    // wave's DS operations execute in order, so the reads of those units precede the writes and
+    // only one pair of results is live
+    MARK(mfma);
 #pragma unroll
-      for (int fb = 0; fb < BW; ++fb) {
+    for (int fp = 0; fp < BW / 2; ++fp) {
+      float2 ybuf[2][NT];
+      f32x4 acc[2][NT];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int fb = 2 * fp + h;
         const int f = wave * BW + fb;
-        f32x4 acc[NT];
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int nt = 0; nt < NT; ++nt) acc[h][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           uint4 raw = araw[fb][ks];
           if (ABLATE(64)) {
           } else if (f == 0) {
-            raw.x &= a_bin0; raw.y &= a_bin0; raw.z &= a_bin0; raw.w &= a_bin0;
+            raw.x = pkmul(raw.x, amul0[ks]); raw.y = pkmul(raw.y, amul0[ks]);
+            raw.z = pkmul(raw.z, amul0[ks]); raw.w = pkmul(raw.w, amul0[ks]);
           } else {
-            raw.x = __builtin_amdgcn_perm(raw.x, raw.x, a_sel) ^ a_xor;
-            raw.y = __builtin_amdgcn_perm(raw.y, raw.y, a_sel) ^ a_xor;
-            raw.z = __builtin_amdgcn_perm(raw.z, raw.z, a_sel) ^ a_xor;
-            raw.w = __builtin_amdgcn_perm(raw.w, raw.w, a_sel) ^ a_xor;
+            raw.x = pkmul(__builtin_amdgcn_perm(raw.x, raw.x, a_sel), amul[ks]);
+            raw.y = pkmul(__builtin_amdgcn_perm(raw.y, raw.y, a_sel), amul[ks]);
+            raw.z = pkmul(__builtin_amdgcn_perm(raw.z, raw.z, a_sel), amul[ks]);
+            raw.w = pkmul(__builtin_amdgcn_perm(raw.w, raw.w, a_sel), amul[ks]);
           }
           const f16x8 a = __builtin_bit_cast(f16x8, raw);
           if (ABLATE(1)) {
@@ -498,52 +537,47 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
           }
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt)
-            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, creg[fb][ks][nt], acc[nt], 0, 0, 0);
+            acc[h][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, creg[fb][ks][nt], acc[h][nt], 0, 0, 0);
         }
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt)            // rows 4t + {re hi, re lo, im hi, im lo}
-          ybuf[fb][nt] = make_float2(acc[nt][0] + acc[nt][1], acc[nt][2] + acc[nt][3]);
+        for (int nt = 0; nt < NT; ++nt)             // rows 4 yt + {re hi, re lo, im hi, im lo}
+          ybuf[h][nt] = make_float2((acc[h][nt][0] + acc[h][nt][1]) * ry, (acc[h][nt][2] + acc[h][nt][3]) * ry);
       }
-      // own A bins were all read (wave-local DS order): Y pairs go over them, 16 B per lane
-      MARK(ywrite);
-      wave_lds_sync();
-      const int yt = mlane >> 4;
+      const int p = (wave * BW) / 2 + fp;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const int R = yt * G::NOG + nt * 16 + (mlane & 15);
-#pragma unroll
-        for (int fp = 0; fp < BW / 2; ++fp) {
-          const int pr = (wave * BW) / 2 + fp;
-          *reinterpret_cast<float4*>(aimg + yunit(pr, R)) =
-              make_float4(ybuf[2 * fp][nt].x, ybuf[2 * fp][nt].y, ybuf[2 * fp + 1][nt].x, ybuf[2 * fp + 1][nt].y);
-        }
+        *reinterpret_cast<float4*>(region + (R / RPWI) * SLOT + yunit(p, R % RPWI)) =
+            make_float4(ybuf[0][nt].x, ybuf[0][nt].y, ybuf[1][nt].x, ybuf[1][nt].y);
       }
     }
-    STAMP(sb + 4);
-    lds_barrier();                                  // B4: Y image complete
-    STAMP(sb + 5);
+    MARK(ywrite);
+  };
 
+  // ---- inverse of one M-tile (wave w < NWI, slot w): Y rows -> y rows staged in the slot
+  auto inverse = [&](char* region) {
     MARK(inv_read);
-    // ---- inverse transforms -> y rows staged in this tile's region (stored next tile)
-    if (inv_active) {
-      const int ptid = opaque(tid);
-      const int grp = (int)((unsigned)ptid / L), g = ptid & (L - 1);
-      const int k1 = k1_of<L>(g);
-      const int R = inv_row(grp);
-      const int inv_t = R >> 5, inv_o = R & (G::NOG - 1);
-      // Y[k], k = g + L n2: unit (g >> 1) + (L/2) n2, half g & 1. Y[H-k] = (H-L-L n2) + (L-g):
-      // unit (H-L)/2 - (L/2) n2 + ((L-g) >> 1), half (L-g) & 1 (k = 0 reads past the image,
-      // unused: bin 0 is packed). Swizzle bit p & SWM is lane-constant in both.
-      const int gl = L - g;
-      const char* ykb = region + yunit(g >> 1, R) + 8 * (g & 1);
-      const char* yhb = region + yunit(gl >> 1, R) + 8 * (gl & 1);
-      float2 yk[16], yh[16], wk[16];
+    const int ptid = opaque(tid);
+    const int gi = (int)((unsigned)(ptid & 63) / L), g = ptid & (L - 1);
+    const int k1 = k1_of<L>(g);
+    const int r = inv_row(gi);
+    const int R = wave * RPWI + r;                  // token R >> 5, output block R & 31
+    const int inv_o = R & (G::NOG - 1);
+    char* slot = region + wave * SLOT;
+    // Y[k], k = g + L n2: unit (g >> 1) + (L/2) n2, half g & 1. Y[H-k] = (H-L-L n2) + (L-g):
+    // unit (H-L)/2 - (L/2) n2 + ((L-g) >> 1), half (L-g) & 1 (k = 0 reads past the slot,
+    // unused: bin 0 is packed). The swizzle bit p & SWM is lane-constant in both.
+    const int gl = L - g;
+    const char* ykb = slot + yunit(g >> 1, r) + 8 * (g & 1);
+    const char* yhb = slot + yunit(gl >> 1, r) + 8 * (gl & 1);
+    float2 v[16];
+    float2 yk[16], yh[16], wk[16];
 #pragma unroll
-      for (int hb = 0; hb < 2; ++hb) {
+    for (int hb = 0; hb < 2; ++hb) {
 #pragma unroll
       for (int n2 = 8 * hb; n2 < 8 * hb + 8; ++n2) {
-        yk[n2] = *reinterpret_cast<const float2*>(ykb + n2 * (L / 2) * PS);
-        yh[n2] = *reinterpret_cast<const float2*>(yhb + ((H - L) / 2 - (L / 2) * n2) * PS);
+        yk[n2] = *reinterpret_cast<const float2*>(ykb + n2 * (L / 2) * RPWI * 16);
+        yh[n2] = *reinterpret_cast<const float2*>(yhb + ((H - L) / 2 - (L / 2) * n2) * RPWI * 16);
         wk[n2] = twb[g + L * n2];
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -558,77 +592,104 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
         if (n2 == 0 && g == 0) z = make_float2(yk[0].x + yk[0].y, yk[0].x - yk[0].y);   // packed bin 0
         v[n2] = z;
       }
+    }
+    MARK(inv_dft);
+    float2 tw[16];
+#pragma unroll
+    for (int k2 = 1; k2 < 16; ++k2) tw[k2] = twi[g * G::TS + k2];
+    if (!ABLATE(8)) {
+      dft<16, true>(v);
+#pragma unroll
+      for (int k2 = 1; k2 < 16; ++k2) v[k2] = cmul(v[k2], tw[k2]);
+      lane_dft<L, true>(v, g);
+    }
+    MARK(inv_out);
+    // y[32 k1 + 2 k2 + {0,1}] = D (R0, R1) / s_C, D = stat_decode<L, true>(g)
+    const float sc = inv_sc;
+    const bool rot = L == 4 && g == 3;              // stored = -i z
+    const float sd = (g == 1 || g == 2) ? -sc : sc;
+    const float c00 = rot ? 0.f : sd, c01 = rot ? -sc : 0.f;
+    const float c10 = rot ? sc : 0.f, c11 = rot ? 0.f : sd;
+    const float* brow = bias_l + inv_o * B + 32 * k1;
+    // piece j of this lane's run (unit k1 NQL + j) goes to row sx ^ hmap(j), sx = r ^ hmap(k1 NQL)
+    const int sx = r ^ hmap(k1 * NQL);
+    char* stb = slot + 16 * (k1 * NQL * RPWI);
+    auto stage = [&](int j) { return stb + 16 * (j * RPWI + (sx ^ hmap(j) ^ (j & SWM))); };
+    wave_lds_sync();                                // the wave's Y reads precede its y writes
+    // 8 outputs (4 registers) per step: .to(x.dtype) :266, + bias :270-271, .to(y dtype)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float o8[8];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const float2 z = v[4 * q + h];
+        o8[2 * h] = fmaf(c00, z.x, c01 * z.y);
+        o8[2 * h + 1] = fmaf(c10, z.x, c11 * z.y);
       }
-      MARK(inv_dft);
-      float2 tw[16];
-#pragma unroll
-      for (int k2 = 1; k2 < 16; ++k2) tw[k2] = twi[g * G::TS + k2];
-      if (!ABLATE(8)) {
-        dft<16, true>(v);
-#pragma unroll
-        for (int k2 = 1; k2 < 16; ++k2) v[k2] = cmul(v[k2], tw[k2]);
-        lane_dft<L, true>(v, g);
-      }
-      MARK(inv_out);
-      // y[32 k1 + 2 k2 + {0,1}] = D (R0, R1) / (s_t s_C), D = stat_decode<L, true>(g)
-      const int e_t = __builtin_amdgcn_frexp_expf(__uint_as_float(slot[inv_t]));
-      int nsc = 15 - e_t;
-      nsc = nsc < -126 ? -126 : (nsc > 127 ? 127 : nsc);
-      const float sc = __int_as_float((127 - nsc) << 23) * inv_sc;
-      const bool rot = L == 4 && g == 3;                     // stored = -i z
-      const float sd = (g == 1 || g == 2) ? -sc : sc;
-      const float c00 = rot ? 0.f : sd, c01 = rot ? -sc : 0.f;
-      const float c10 = rot ? sc : 0.f, c11 = rot ? 0.f : sd;
-      const float* brow = bias_l + inv_o * B + 32 * k1;
-      // piece j of this lane's run (unit k1 NQL + j) goes to row X ^ hmap(j), X = R ^ hmap(k1 NQL)
-      const int sx = R ^ hmap(k1 * NQL);
-      char* stb = region + k1 * NQL * PS;
-      auto stage = [&](int j) { return stb + j * PS + 16 * (sx ^ hmap(j) ^ (j & SWM)); };
-      wave_lds_sync();                               // the wave's Y reads precede its y writes
-      // 8 outputs (4 registers) per step: .to(x.dtype) :266, + bias :270-271, .to(y dtype)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float o8[8];
+      // a 16-bit y without bias is ONE rounding (round_to then the cast is the same value)
+      if (Y32 || bias_dt != BCFFT_NONE) {
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
-          const float2 z = v[4 * q + h];
-          o8[2 * h] = fmaf(c00, z.x, c01 * z.y);
-          o8[2 * h + 1] = fmaf(c10, z.x, c11 * z.y);
+          const float2 rr = round_pair<XT>(o8[2 * h], o8[2 * h + 1]);
+          o8[2 * h] = rr.x;
+          o8[2 * h + 1] = rr.y;
         }
-        // a 16-bit y without bias is ONE rounding (round_to then the cast is the same value)
-        if (Y32 || bias_dt != BCFFT_NONE) {
-#pragma unroll
-          for (int h = 0; h < 4; ++h) {
-            const float2 r = round_pair<XT>(o8[2 * h], o8[2 * h + 1]);
-            o8[2 * h] = r.x;
-            o8[2 * h + 1] = r.y;
-          }
-          if (bias_dt != BCFFT_NONE) {
-            const float4 b0 = *reinterpret_cast<const float4*>(brow + 8 * q);
-            const float4 b1 = *reinterpret_cast<const float4*>(brow + 8 * q + 4);
-            o8[0] += b0.x; o8[1] += b0.y; o8[2] += b0.z; o8[3] += b0.w;
-            o8[4] += b1.x; o8[5] += b1.y; o8[6] += b1.z; o8[7] += b1.w;
-          }
-        }
-        if constexpr (Y32) {
-#pragma unroll
-          for (int hq = 0; hq < 2; ++hq) {
-            *reinterpret_cast<float4*>(stage(2 * q + hq)) =
-                make_float4(o8[4 * hq], o8[4 * hq + 1], o8[4 * hq + 2], o8[4 * hq + 3]);
-          }
-        } else {
-          *reinterpret_cast<uint4*>(stage(q)) =
-              make_uint4(pack16<XT>(o8[0], o8[1]), pack16<XT>(o8[2], o8[3]), pack16<XT>(o8[4], o8[5]),
-                         pack16<XT>(o8[6], o8[7]));
+        if (bias_dt != BCFFT_NONE) {
+          const float4 b0 = *reinterpret_cast<const float4*>(brow + 8 * q);
+          const float4 b1 = *reinterpret_cast<const float4*>(brow + 8 * q + 4);
+          o8[0] += b0.x; o8[1] += b0.y; o8[2] += b0.z; o8[3] += b0.w;
+          o8[4] += b1.x; o8[5] += b1.y; o8[6] += b1.z; o8[7] += b1.w;
         }
       }
+      if constexpr (Y32) {
+#pragma unroll
+        for (int hq = 0; hq < 2; ++hq)
+          *reinterpret_cast<float4*>(stage(2 * q + hq)) =
+              make_float4(o8[4 * hq], o8[4 * hq + 1], o8[4 * hq + 2], o8[4 * hq + 3]);
+      } else {
+        *reinterpret_cast<uint4*>(stage(q)) =
+            make_uint4(pack16<XT>(o8[0], o8[1]), pack16<XT>(o8[2], o8[3]), pack16<XT>(o8[4], o8[5]),
+                       pack16<XT>(o8[6], o8[7]));
+      }
     }
+  };
+
+  // Pipeline, two workgroup barriers per M-tile. Iteration it (region R = R[it & 1] holds tile
+  // m, R' = the other holds tile m - gstride):
+  //   P1  inverse of tile m - gstride (slot w of R' -> y rows staged there), their stores, then
+  //       the LDS-DMA of x(m + gstride) into slot w of R' (private to wave w from here on: no
+  //       barrier needed, and the DMA gets a whole period of lead), then the forward of tile m
+  //       in slot w of R, whose counted vmcnt wait leaves those stores and DMA in flight | Ba |
+  //   P2  MFMAs of tile m: A fragments in R -> Y units in R                          | Bb |
+  // (Measured alternatives: issuing the stores and DMA inside the forward, after its x reads,
+  // and running inverse / forward in opposite orders on SIMD mates were both slower.)
+  const bool fwd_active = wave < NWF, inv_active = wave < NWI;
+  int64_t m = blockIdx.x;
+  STAMP(0);
+  if (m < n_mtiles && !ABLATE(16)) dma_tile(m, lds);
+  for (int it = 0; m < n_mtiles || it > 0; ++it, m += gstride) {
+    char* region = lds + (it & 1) * G::REGION;
+    char* other = lds + ((it + 1) & 1) * G::REGION;
+    const bool have_f = m < n_mtiles;
+    const bool st = it > 0 && inv_active;
+    const bool dm = m + gstride < n_mtiles && fwd_active && !ABLATE(16);
+    const int sb = 1 + 7 * (it & 7);
+    STAMP(sb);
+    if (st) inverse(other);
+    STAMP(sb + 1);
+    MARK(store);
+    if (st) store_tile(m - gstride, other);
+    if (dm) dma_tile(m + gstride, other);
+    STAMP(sb + 2);
+    if (!have_f) break;
+    if (fwd_active) forward(region, (st ? NST : 0) + (dm ? NDMA : 0));
+    STAMP(sb + 3);
+    lds_barrier();                                  // Ba: A fragments and scales complete
+    STAMP(sb + 4);
+    cmac(region);
+    STAMP(sb + 5);
+    lds_barrier();                                  // Bb: Y image complete
     STAMP(sb + 6);
-  }
-  // the last tile's stores (each wave its own staged rows: wave-local LDS order suffices)
-  if (it > 0) {
-    wave_lds_sync();
-    store_tile(m - gstride, lds + ((it + 1) & 1) * G::REGION);
   }
   STAMP(63);
 }

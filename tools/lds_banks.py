@@ -50,7 +50,9 @@ def row_of(G, gr, pi):
 
 
 def yaddr(G, p, R):
-    return p * G["PS"] + 16 * (R ^ (p & G["SWM"]))
+    """slot layout: row R's units live in slot R // RPWI (the inverse wave's own slot)"""
+    r = R % G["RPW"]
+    return (R // G["RPW"]) * 8192 + 16 * (p * G["RPW"] + (r ^ (p & G["SWM"])))
 
 
 def k1_of(G, j):
@@ -156,6 +158,77 @@ KNOWN = {(128, 4): ([0, 2, 1, 3, 4, 6, 5, 7], [5, 8, 0, 1, 2]),
          (64, 4): (ID16, [1, 2, 4, 12]),
          (64, 2): (ID16, [1, 4, 12])}
 
+# ---------------------------------------------------------------- slot layout (2-barrier pipeline)
+# Region = slots of 8 KiB (yaddr above is already this layout's Y addressing). Slot s: forward wave s's x rows, then its A fragments (unit
+# U(f, prec, lq) = f*2NQ + prec*NQ + lq, XOR ((f >> 4) ^ tsw(s)) << SA), then the Y units of
+# inverse rows [s RPWI, (s+1) RPWI): unit p*RPWI + (r ^ (p & SWM)).
+SLOT = 8192
+
+
+def ageo(b, ni):
+    G = geo(b, 4)
+    G.update(NI=ni, RPWF=64 // G["L"], NQ=(64 // G["L"]) // 4, KS=ni // 16,
+             SA=1 if b == 128 else 2)
+    return G
+
+
+def a_unit(G, s, f, prec, lq, tsw):
+    U = f * 2 * G["NQ"] + prec * G["NQ"] + lq
+    return s * SLOT + 16 * (U ^ (((f >> 4) ^ tsw[s]) << G["SA"]))
+
+
+def a_writes(G, tsw):
+    L, worst = G["L"], 1
+    for s in range(4 * G["NI"] // G["RPWF"]):
+        for k2 in range(16):
+            for prec in range(2):
+                ad = []
+                for lane in range(64):
+                    li, g = lane // L, lane % L
+                    f = k2 + 16 * k1_of(G, g)
+                    ad.append(a_unit(G, s, f, prec, li >> 2, tsw) + 4 * (li & 3))
+                worst = max(worst, cycles(ad, 4, RD64, 32))     # ds_write_b32: 2 x 32 lanes, mod 32
+    return worst
+
+
+def a_reads(G, tsw):
+    worst = 1
+    for f in range(G["H"]):
+        for ks in range(G["KS"]):
+            ad = []
+            for lane in range(64):
+                arow, kb = lane & 15, lane >> 4
+                t, prec = arow >> 2, arow & 1
+                row0 = t * G["NI"] + 16 * ks
+                s, lq = row0 // G["RPWF"], (row0 % G["RPWF"]) // 4 + kb
+                ad.append(a_unit(G, s, f, prec, lq, tsw))
+            worst = max(worst, cycles(ad, 16, RD128, 64))
+    return worst
+
+
+def a_search(G):
+    ns = 4 * G["NI"] // G["RPWF"]
+    best = None
+    for tsw in itertools.product(range(4), repeat=ns):
+        w = (a_writes(G, tsw), a_reads(G, tsw))
+        if best is None or sum(w) < sum(best[1]):
+            best = (tsw, w)
+        if w == (1, 1):
+            break
+    return best
+
+
+def slot_check():
+    bad = False
+    for b, ni in ((128, 32), (64, 32), (64, 64)):
+        G = ageo(b, ni)
+        tsw, w = a_search(G)
+        ok = w == (1, 1)
+        bad |= not ok
+        print(f"slot layout b={b} NI={ni}: tsw={list(tsw)} A writes {w[0]}, A reads {w[1]} {'OK' if ok else 'CONFLICTS'}")
+    return bad
+
+
 if __name__ == "__main__":
     bad = False
     for b, es in ((128, 4), (128, 2), (64, 4), (64, 2)):
@@ -168,4 +241,5 @@ if __name__ == "__main__":
         ok = max(w.values()) == 1
         bad |= not ok
         print(f"b={b} ES_y={es}: row map pi={pi} staging XOR columns={cols} -> {w} {'OK' if ok else 'CONFLICTS'}")
+    bad |= slot_check()
     sys.exit(1 if bad else 0)

@@ -3,9 +3,8 @@
 Loads lib/libbcfft_ablate.so (`make -C llama-fft_amd ablate`), or with TIMELINE_BUILD=stamps
 lib/libbcfft_stamps.so (`make stamps`: stamps only, the product's control flow, no switches). Every wave stamps s_memtime at
 the STAMP points of bc_forward_stat_kernel (bcfft_stat.hip):
-  0 start | per M-tile it (base 1 + 7 (it % 8)): +0 loop top, +1 own x rows landed,
-  +2 after B1 (forward + untangle + token max), +3 after B2 (split, A image, previous stores),
-  +4 DMA + MFMAs + Y pairs written, +5 after B4, +6 inverse + y staged | 63 end
+  0 start | per M-tile it (base 1 + 7 (it % 8)): +0 loop top, +1 inverse done, +2 stores and
+  next DMA issued, +3 forward done, +4 after barrier Ba, +5 MFMAs + Y written, +6 after Bb | 63 end
 and the phase switches (outputs are WRONG when set) time what each phase costs.
 usage: python tools/timeline_stat.py [K M B IO N]
 """
@@ -23,7 +22,7 @@ sys.path.insert(0, os.path.join(ROOT, "llama-fft_amd"))
 import torch  # noqa: E402
 from bcfft import _lib, ops  # noqa: E402
 
-SEG = ["wait x", "fwd->B1", "split+st->B2", "dma+mfma+Y", "B4 wait", "inverse"]
+SEG = ["inverse", "stores+dma", "forward", "Ba wait", "cmac", "Bb wait"]
 FLAGS = {"full": 0, "no_mfma": 1, "no_store": 2, "no_fwdfft": 4, "no_invfft": 8, "no_xdma": 16,
          "no_mem": 18, "no_fft": 12, "no_fft_no_mem": 30, "no_mem_no_aread": 18 | 32,
          "no_mem_no_atrans": 18 | 64, "no_mem_no_a_no_mfma": 18 | 32 | 64 | 1}
