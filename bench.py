@@ -76,27 +76,30 @@ def make_layer(k, m, b, io, bias, dev, seed=1):
 
 
 def time_layer(layer, x, steps, warmup, barrier=None):
-    """Returns (wall ms per step over the bracketed region, mean kernel ms from events)."""
+    """Returns (wall ms per step over the bracketed region, mean kernel ms per launch from HIP
+    events). One event pair brackets all K back-to-back launches on the launch stream: a pair
+    around EACH launch adds its own marker latency (~6 us per step measured on MI355X, see
+    tools/event_timing.py), while K launches back to back give the launch duration plus the
+    inter-kernel gap, within ~2-3 % of rocprofv3's per-kernel average."""
     stream = torch.cuda.current_stream()
     with torch.inference_mode():
         layer._spectra(layer.c)                                # spectra outside timing
         for _ in range(warmup):
             layer(x)
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(steps)]
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         if barrier:
             barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for s, e in ev:
-            s.record(stream)
+        s.record(stream)
+        for _ in range(steps):
             layer(x)
-            e.record(stream)
+        e.record(stream)
         torch.cuda.synchronize()
         if barrier:
             barrier()
         wall = (time.perf_counter() - t0) * 1e3 / steps
-    kern = sum(s.elapsed_time(e) for s, e in ev) / steps
+    kern = s.elapsed_time(e) / steps
     return wall, kern
 
 

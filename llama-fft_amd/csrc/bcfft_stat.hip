@@ -214,10 +214,58 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp_o = blockIdx.y;                    // output group
+  // 1-D grid, one workgroup per CU: workgroup i serves output group i % groups and, with the
+  // other workgroups of that group, strides over the M-tiles
+  const int n_groups = (n_out + G::NOG - 1) / G::NOG;
+  const int grp_o = blockIdx.x % n_groups;         // output group
+  const int wg_in_grp = blockIdx.x / n_groups;
   const int64_t M = (int64_t)n_out * B;
   const int64_t n_mtiles = (n_tokens + TT - 1) / TT;
-  const int gstride = gridDim.x;
+  const int gstride = (gridDim.x - grp_o + n_groups - 1) / n_groups;   // workgroups of this group
+
+  // ---- LDS region layout: NWF slots of 8 KiB. Slot s belongs to forward wave s: that wave's
+  // x rows land there (LDS-DMA), its forward replaces them in place by its A fragments (no other
+  // wave reads or writes the slot in that phase), and after the MFMAs slot s holds the Y units of
+  // the inverse rows [s RPWI, (s+1) RPWI), which inverse wave s reads, replaces by its staged y
+  // rows and stores. Bank proofs of every access: tools/lds_banks.py.
+  constexpr int SLOT = 8192;
+  constexpr int NQ = RPWF / 4;                     // block quads per slot
+  constexpr int NWF = FWD_ROWS / RPWF;             // forward waves = A slots
+  constexpr int RPWI = 64 / L;                     // inverse rows per wave
+  constexpr int NWI = INV_ROWS / RPWI;             // inverse waves = Y slots
+  constexpr int SA = L == 4 ? 1 : 2;               // A swizzle shift: log2(8 / L)
+  constexpr int SWM = L / 2 - 1;                   // Y swizzle mask
+  static_assert(RPWF * H * 8 == SLOT && RPWI * (H / 2) * 16 == SLOT, "slot = A rows = Y rows");
+  static_assert(RPWF * RB <= SLOT && NWF * SLOT <= G::REGION && NWI <= NWF, "slots");
+  static_assert(NI % RPWF == 0 || RPWF % NI == 0, "a forward wave's rows are one token");
+  int* wsc = reinterpret_cast<int*>(slots);        // per forward wave: its scale exponent
+
+  // ---- x M-tile -> region by LDS-DMA: forward wave w loads its own RPWF rows (NDMA 1-KiB
+  // pieces) into slot w, so its own vmcnt wait is all it needs before reading them. The tile's
+  // 4 token rows are one contiguous span of x: a lane's source offset is its row byte with the
+  // row's unit swizzle (swz_x) XORed in; the buffer range check zero-fills rows past n_tokens
+  // (those tokens are never stored).
+  auto dma_tile = [&](int64_t m, char* region) {
+    if (wave >= NWF) return;
+    const int64_t tok0 = m * TT;
+    const int64_t ntok = n_tokens - tok0 < TT ? n_tokens - tok0 : TT;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>((const char*)xv) + tok0 * K * ES, 0, (int)(ntok * K * ES), 0x00020000);
+    const int dlane = opaque(lane);
+#pragma unroll
+    for (int q = 0; q < NDMA; ++q) {
+      const int byte = (wave * NDMA + q) * 1024 + dlane * 16;
+      const int voff = byte ^ (swz_x<L, ES>(byte / RB) << 4);
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(region + wave * SLOT + q * 1024));
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(voff), "s"(xrs), "s"(dst) : "memory");
+    }
+  };
+  // the first M-tile's x goes out before anything else: it lands under the tables and the
+  // 256 KiB of stationary weight loads
+  if (wg_in_grp < n_mtiles && !ABLATE(16)) dma_tile(wg_in_grp, lds);
+
 
   // ---- tables (fp64 trig, once per workgroup)
   for (int e = tid; e < L * 16; e += G::NTHR) {
@@ -250,15 +298,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     twb[k] = make_float2((float)cs, (float)-sn);
   }
   if (tid < 8) slots[tid] = 0u;
-  // the group's bias as fp32 in LDS, so no VMEM load sits in the loop: a waited load would
-  // also drain every older y store and x DMA (vmcnt retires in order)
-  float* bias_l = reinterpret_cast<float*>(lds + G::BIAS_OFF);
-  if (bias_dt != BCFFT_NONE) {
-    for (int e = tid; e < G::NOG * B; e += G::NTHR) {
-      const int64_t col = (int64_t)grp_o * G::NOG * B + e;
-      bias_l[e] = col < (int64_t)n_out * B ? load_scalar(bias, col, bias_dt) : 0.f;
-    }
-  }
   lds_barrier();                                   // tables before the weight loads (pressure)
 
   // ---- stationary B fragments: conj(C) * s_C as fp16, K/32 VGPRs per lane
@@ -274,23 +313,17 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
         for (int nt = 0; nt < NT; ++nt)
           creg[fb][ks][nt] = __builtin_bit_cast(f16x8, img[((fb * KS + ks) * NT + nt) * 64]);
   }
+  // the group's bias as fp32 in LDS, so no VMEM load sits in the loop: a waited load would
+  // also drain every older y store and x DMA (vmcnt retires in order). Read after the weight
+  // loads are issued, so its waits overlap theirs and the first DMA's.
+  float* bias_l = reinterpret_cast<float*>(lds + G::BIAS_OFF);
+  if (bias_dt != BCFFT_NONE) {
+    for (int e = tid; e < G::NOG * B; e += G::NTHR) {
+      const int64_t col = (int64_t)grp_o * G::NOG * B + e;
+      bias_l[e] = col < (int64_t)n_out * B ? load_scalar(bias, col, bias_dt) : 0.f;
+    }
+  }
 
-  // ---- LDS region layout: NWF slots of 8 KiB. Slot s belongs to forward wave s: that wave's
-  // x rows land there (LDS-DMA), its forward replaces them in place by its A fragments (no other
-  // wave reads or writes the slot in that phase), and after the MFMAs slot s holds the Y units of
-  // the inverse rows [s RPWI, (s+1) RPWI), which inverse wave s reads, replaces by its staged y
-  // rows and stores. Bank proofs of every access: tools/lds_banks.py.
-  constexpr int SLOT = 8192;
-  constexpr int NQ = RPWF / 4;                     // block quads per slot
-  constexpr int NWF = FWD_ROWS / RPWF;             // forward waves = A slots
-  constexpr int RPWI = 64 / L;                     // inverse rows per wave
-  constexpr int NWI = INV_ROWS / RPWI;             // inverse waves = Y slots
-  constexpr int SA = L == 4 ? 1 : 2;               // A swizzle shift: log2(8 / L)
-  constexpr int SWM = L / 2 - 1;                   // Y swizzle mask
-  static_assert(RPWF * H * 8 == SLOT && RPWI * (H / 2) * 16 == SLOT, "slot = A rows = Y rows");
-  static_assert(RPWF * RB <= SLOT && NWF * SLOT <= G::REGION && NWI <= NWF, "slots");
-  static_assert(NI % RPWF == 0 || RPWF % NI == 0, "a forward wave's rows are one token");
-  int* wsc = reinterpret_cast<int*>(slots);        // per forward wave: its scale exponent
 
   // A fragment unit (16 B: 4 blocks x (re, im) fp16 of bin f, precision prec, block quad lq)
   // within slot s; the XOR keeps the lanes of the forward's writes and of the MFMA reads on
@@ -327,28 +360,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     return r;
   };
 
-  // ---- x M-tile -> region by LDS-DMA: forward wave w loads its own RPWF rows (NDMA 1-KiB
-  // pieces) into slot w, so its own vmcnt wait is all it needs before reading them. The tile's
-  // 4 token rows are one contiguous span of x: a lane's source offset is its row byte with the
-  // row's unit swizzle (swz_x) XORed in; the buffer range check zero-fills rows past n_tokens
-  // (those tokens are never stored).
-  auto dma_tile = [&](int64_t m, char* region) {
-    if (wave >= NWF) return;
-    const int64_t tok0 = m * TT;
-    const int64_t ntok = n_tokens - tok0 < TT ? n_tokens - tok0 : TT;
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<char*>((const char*)xv) + tok0 * K * ES, 0, (int)(ntok * K * ES), 0x00020000);
-    const int dlane = opaque(lane);
-#pragma unroll
-    for (int q = 0; q < NDMA; ++q) {
-      const int byte = (wave * NDMA + q) * 1024 + dlane * 16;
-      const int voff = byte ^ (swz_x<L, ES>(byte / RB) << 4);
-      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(region + wave * SLOT + q * 1024));
-      uint32_t keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep) : "v"(voff), "s"(xrs), "s"(dst) : "memory");
-    }
-  };
 
   // the inverse wave stores the rows it staged, in global order, RPI whole rows (1 KiB) per
   // instruction: rows r0 + q RPI of its slot, r0 = lane / NPR
@@ -664,16 +675,18 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
   // (Measured alternatives: issuing the stores and DMA inside the forward, after its x reads,
   // and running inverse / forward in opposite orders on SIMD mates were both slower.)
   const bool fwd_active = wave < NWF, inv_active = wave < NWI;
-  int64_t m = blockIdx.x;
+#ifdef STAT_PRIO
+  if (wave >= 4) __builtin_amdgcn_s_setprio(STAT_PRIO);   // second-dispatched half wins arbitration
+#endif
+  int64_t m = wg_in_grp;
   STAMP(0);
-  if (m < n_mtiles && !ABLATE(16)) dma_tile(m, lds);
   for (int it = 0; m < n_mtiles || it > 0; ++it, m += gstride) {
     char* region = lds + (it & 1) * G::REGION;
     char* other = lds + ((it + 1) & 1) * G::REGION;
     const bool have_f = m < n_mtiles;
     const bool st = it > 0 && inv_active;
     const bool dm = m + gstride < n_mtiles && fwd_active && !ABLATE(16);
-    const int sb = 1 + 7 * (it & 7);
+    const int sb = 1 + 7 * (it < 7 ? it : 7);       // stamp slots: iterations 0-6, then the latest
     STAMP(sb);
     if (st) inverse(other);
     STAMP(sb + 1);
@@ -782,14 +795,14 @@ void launch_stat(const void* x, int64_t n, int n_out, const void* spec, const vo
                  void* y, hipStream_t s) {
   const bcfft::SpecLayout sl = bcfft::spec_layout(n_out, 16 * KS, B);
   const int groups = sl.stat_groups;
-  // one workgroup per CU; the groups of one token slice share an XCD (stride multiple of 8)
-  int gx = cu_count() / groups;
-  if (gx >= 8) gx -= gx % 8;
-  if (gx < 1) gx = 1;
+  // one workgroup per CU (1-D grid, group = index % groups): every group gets cus/groups
+  // workgroups, rounded either way, instead of a whole-XCD multiple (11 groups: 253 vs 176)
   const int64_t n_mtiles = (n + 3) / 4;
-  if (gx > n_mtiles) gx = (int)n_mtiles;
+  int64_t total = cu_count();
+  if (total > groups * n_mtiles) total = groups * n_mtiles;
+  if (total < groups) total = groups;
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
-  hipLaunchKernelGGL((bcfft::bc_forward_stat_kernel<B, KS, XT, YF32>), dim3(gx, groups), dim3(512), 0, s,
+  hipLaunchKernelGGL((bcfft::bc_forward_stat_kernel<B, KS, XT, YF32>), dim3((unsigned)total), dim3(512), 0, s,
                      x, n, n_out, stat, bias, bias_dt, y);
 }
 

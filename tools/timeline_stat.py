@@ -3,7 +3,7 @@
 Loads lib/libbcfft_ablate.so (`make -C llama-fft_amd ablate`), or with TIMELINE_BUILD=stamps
 lib/libbcfft_stamps.so (`make stamps`: stamps only, the product's control flow, no switches). Every wave stamps s_memtime at
 the STAMP points of bc_forward_stat_kernel (bcfft_stat.hip):
-  0 start | per M-tile it (base 1 + 7 (it % 8)): +0 loop top, +1 inverse done, +2 stores and
+  0 start | per M-tile it (base 1 + 7 min(it, 7)): +0 loop top, +1 inverse done, +2 stores and
   next DMA issued, +3 forward done, +4 after barrier Ba, +5 MFMAs + Y written, +6 after Bb | 63 end
 and the phase switches (outputs are WRONG when set) time what each phase costs.
 usage: python tools/timeline_stat.py [K M B IO N]
