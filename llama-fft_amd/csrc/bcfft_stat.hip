@@ -252,14 +252,24 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<char*>((const char*)xv) + tok0 * K * ES, 0, (int)(ntok * K * ES), 0x00020000);
     const int dlane = opaque(lane);
+    // piece q's source offset = (wave NDMA + q) KiB + lane's 16 B, with the row's unit swizzle
+    // XORed in. The swizzle sees row & 15 only and the wave's first row is a multiple of 16, so
+    // it repeats with period DP in q: DP lane bases, q KiB in soffset. (Not the instruction
+    // offset: on an LDS-DMA load that offset moves the LDS destination too. soffset is outside
+    // the range check, which stays right: a wave's rows are whole tokens, so its lane base
+    // alone is in or out of the tile's token range.)
+    constexpr int RPK = 1024 / RB;                 // x rows per KiB
+    constexpr int DP = 16 / RPK < NDMA ? 16 / RPK : NDMA;
+    int vb[DP];
+#pragma unroll
+    for (int c = 0; c < DP; ++c)
+      vb[c] = wave * NDMA * 1024 + ((dlane * 16) ^ (swz_x<L, ES>(c * RPK + (dlane * 16) / RB) << 4));
 #pragma unroll
     for (int q = 0; q < NDMA; ++q) {
-      const int byte = (wave * NDMA + q) * 1024 + dlane * 16;
-      const int voff = byte ^ (swz_x<L, ES>(byte / RB) << 4);
       const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(region + wave * SLOT + q * 1024));
       uint32_t keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep) : "v"(voff), "s"(xrs), "s"(dst) : "memory");
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(vb[q % DP]), "s"(xrs), "s"(dst), "s"(q * 1024) : "memory");
     }
   };
   // the first M-tile's x goes out before anything else: it lands under the tables and the
@@ -377,11 +387,21 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     const int o0 = rho0 & (G::NOG - 1);
     const int yoff0 = (int)((((int64_t)(rho0 >> 5) * M) + (int64_t)(grp_o * G::NOG + o0) * B) * ESY) + 16 * pc;
     const int nvalid = n_out - grp_o * G::NOG;      // output blocks of this group that exist
+    uint4 d[NST];                                   // all staged reads first: one LDS latency
 #pragma unroll
-    for (int q = 0; q < NST; ++q) {
-      const uint4 d = *reinterpret_cast<const uint4*>(regn + (src0 ^ (16 * q * RPI)));
-      const int yoff = nvalid >= G::NOG || o0 + q * RPI < nvalid ? yoff0 + q * RPI * B * ESY : 0x7fff0000;
-      if (!ABLATE(2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d), yrs, yoff, 0, 0);
+    for (int q = 0; q < NST; ++q) d[q] = *reinterpret_cast<const uint4*>(regn + (src0 ^ (16 * q * RPI)));
+    __builtin_amdgcn_sched_barrier(0);
+    if (ABLATE(2)) return;
+    if (nvalid >= G::NOG) {                         // uniform: every row of the group exists
+#pragma unroll
+      for (int q = 0; q < NST; ++q)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs, yoff0 + q * RPI * B * ESY, 0, 0);
+    } else {
+#pragma unroll
+      for (int q = 0; q < NST; ++q) {
+        const int yoff = o0 + q * RPI < nvalid ? yoff0 + q * RPI * B * ESY : 0x7fff0000;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs, yoff, 0, 0);
+      }
     }
   };
 
@@ -461,15 +481,18 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     const float s_w = __int_as_float((nsc + 127) << 23);
     MARK(split);
     // hi = fp16(X' s) (round toward zero), lo = fp16(X' s - hi): two fp16 terms ~2^-21
-    char* abase = slot + 4 * (li & 3);
+    // aunit's XOR ((f >> 4) ^ tsw) << SA is lane-constant here (f >> 4 = k1) and stays below
+    // the bin field, so the 32 writes are two per-lane bases plus immediate bin offsets
+    const int ax = (k1 ^ (wave / (NWF / 2))) << SA;
+    char* abase0 = slot + 4 * (li & 3) + 16 * ((li >> 2) ^ ax) + k1 * 16 * (32 * NQ);
+    char* abase1 = slot + 4 * (li & 3) + 16 * ((NQ + (li >> 2)) ^ ax) + k1 * 16 * (32 * NQ);
 #pragma unroll
     for (int k2 = 0; k2 < 16; ++k2) {
       const float ox = xs[k2].x * s_w, oy = xs[k2].y * s_w;
       const f16x2 hi = __builtin_bit_cast(f16x2, __builtin_amdgcn_cvt_pkrtz(ox, oy));
       const f16x2 lo = __builtin_bit_cast(f16x2, __builtin_amdgcn_cvt_pkrtz(ox - (float)hi.x, oy - (float)hi.y));
-      const int f = k2 + 16 * k1;
-      *reinterpret_cast<f16x2*>(abase + aunit(f, 0, li >> 2, wave)) = hi;
-      *reinterpret_cast<f16x2*>(abase + aunit(f, 1, li >> 2, wave)) = lo;
+      *reinterpret_cast<f16x2*>(abase0 + k2 * 16 * (2 * NQ)) = hi;   // = aunit(k2 + 16 k1, 0, li >> 2, wave)
+      *reinterpret_cast<f16x2*>(abase1 + k2 * 16 * (2 * NQ)) = lo;
     }
   };
 
@@ -502,17 +525,23 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
       amul0[ks] = a_reim ? (h << 16) : h;
     }
     const float ry = __int_as_float((127 - nminy) << 23);   // 2^-nsc of the accumulator's token
+    // A fragment of (bin f, K-step ks) = aunit(f, a_prec, lq, s): the wave's bins share f >> 4,
+    // so per K-step one lane base plus an immediate bin offset
+    const char* abase[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int row0 = a_t * NI + 16 * ks;
+      const int s = row0 / RPWF, lq = (row0 % RPWF) / 4 + kb;
+      const int ax = (((wave * BW) >> 4) ^ (s / (NWF / 2))) << SA;
+      abase[ks] = region + s * SLOT + 16 * ((a_prec * NQ + lq) ^ ax) + wave * BW * 16 * (2 * NQ);
+    }
     uint4 araw[BW][KS];                             // every A fragment of the wave's bins, issued
 #pragma unroll                                       // up front in bin order (counted waits)
     for (int fb = 0; fb < BW; ++fb) {
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const int row0 = a_t * NI + 16 * ks;
-        const int s = row0 / RPWF, lq = (row0 % RPWF) / 4 + kb;
-        const int f = wave * BW + fb;
-        araw[fb][ks] = ABLATE(32) ? make_uint4(a_t, kb, f, ks)
-                                  : *reinterpret_cast<const uint4*>(region + s * SLOT + aunit(f, a_prec, lq, s));
-      }
+      for (int ks = 0; ks < KS; ++ks)
+        araw[fb][ks] = ABLATE(32) ? make_uint4(a_t, kb, fb, ks)
+                                  : *reinterpret_cast<const uint4*>(abase[ks] + fb * 16 * (2 * NQ));
     }
     // a bin pair's Y goes over the wave's own A units of those bins once its MFMAs are done: the
     // wave's DS operations execute in order, so the reads of those units precede the writes and
