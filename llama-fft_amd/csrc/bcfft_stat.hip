@@ -115,6 +115,177 @@ __device__ __forceinline__ void lane_dft(float2 (&v)[16], int g) {
   }
 }
 
+// lane_dft with the cross-lane operand read through DPP inside v_fmac_f32 (hipcc emits a separate
+// v_mov_b32_dpp per operand and never folds it): stage A 2, stage B 5 instructions per complex
+// instead of 4 and 6. Same operations in the same order: bit-identical to the C++ form. The
+// s_nop 1 at each end covers the VALU-write -> DPP-read hazard (2 wait states) on the inputs and
+// for the caller's next DPP read; inside, every DPP read is of a register last written >= 2
+// instructions earlier.
+template <int L, bool INV>
+__device__ __forceinline__ void lane_dft_dpp(float2 (&v)[16], int g) {
+  if constexpr (L == 2) {
+    const float s = g ? -1.f : 1.f;
+    asm volatile("s_nop 1\n\t"
+        "v_fmac_f32_dpp %0, %0, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %1, %1, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %2, %2, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %3, %3, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %4, %4, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %5, %5, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %6, %6, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %7, %7, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %8, %8, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %9, %9, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %10, %10, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %11, %11, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %12, %12, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %13, %13, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %14, %14, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %15, %15, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %16, %16, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %17, %17, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %18, %18, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %19, %19, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %20, %20, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %21, %21, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %22, %22, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %23, %23, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %24, %24, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %25, %25, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %26, %26, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %27, %27, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %28, %28, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %29, %29, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %30, %30, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %31, %31, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1"
+        : "+v"(v[0].x), "+v"(v[0].y), "+v"(v[1].x), "+v"(v[1].y), "+v"(v[2].x), "+v"(v[2].y), "+v"(v[3].x), "+v"(v[3].y), "+v"(v[4].x), "+v"(v[4].y), "+v"(v[5].x), "+v"(v[5].y), "+v"(v[6].x), "+v"(v[6].y), "+v"(v[7].x), "+v"(v[7].y), "+v"(v[8].x), "+v"(v[8].y), "+v"(v[9].x), "+v"(v[9].y), "+v"(v[10].x), "+v"(v[10].y), "+v"(v[11].x), "+v"(v[11].y), "+v"(v[12].x), "+v"(v[12].y), "+v"(v[13].x), "+v"(v[13].y), "+v"(v[14].x), "+v"(v[14].y), "+v"(v[15].x), "+v"(v[15].y)
+        : "v"(s));
+  } else {
+    const float sa = g < 2 ? 1.f : -1.f;
+    const float al = g == 0 ? 1.f : (g == 1 ? -1.f : 0.f);
+    const float be = g < 2 ? 0.f : (INV ? -1.f : 1.f);
+    const float mbe = -be;
+    float t;
+    asm volatile("s_nop 1\n\t"
+        "v_fmac_f32_dpp %0, %0, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %1, %1, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %2, %2, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %3, %3, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %4, %4, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %5, %5, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %6, %6, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %7, %7, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %8, %8, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %9, %9, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %10, %10, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %11, %11, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %12, %12, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %13, %13, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %14, %14, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %15, %15, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %16, %16, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %17, %17, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %18, %18, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %19, %19, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %20, %20, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %21, %21, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %22, %22, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %23, %23, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %24, %24, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %25, %25, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %26, %26, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %27, %27, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %28, %28, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %29, %29, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %30, %30, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %31, %31, %33 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %32, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %1, %1, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %1, %0, %36 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %0, %0, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32 %0, %32, %35\n\t"
+        "v_mov_b32_dpp %32, %3 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %3, %3, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %3, %2, %36 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %2, %2, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32 %2, %32, %35\n\t"
+        "v_mov_b32_dpp %32, %5 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %5, %5, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %5, %4, %36 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %4, %4, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32 %4, %32, %35\n\t"
+        "v_mov_b32_dpp %32, %7 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %7, %7, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %7, %6, %36 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %6, %6, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32 %6, %32, %35\n\t"
+        "v_mov_b32_dpp %32, %9 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %9, %9, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %9, %8, %36 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %8, %8, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32 %8, %32, %35\n\t"
+        "v_mov_b32_dpp %32, %11 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %11, %11, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %11, %10, %36 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %10, %10, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32 %10, %32, %35\n\t"
+        "v_mov_b32_dpp %32, %13 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %13, %13, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %13, %12, %36 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %12, %12, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32 %12, %32, %35\n\t"
+        "v_mov_b32_dpp %32, %15 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %15, %15, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %15, %14, %36 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %14, %14, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32 %14, %32, %35\n\t"
+        "v_mov_b32_dpp %32, %17 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %17, %17, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %17, %16, %36 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %16, %16, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32 %16, %32, %35\n\t"
+        "v_mov_b32_dpp %32, %19 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %19, %19, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %19, %18, %36 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %18, %18, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32 %18, %32, %35\n\t"
+        "v_mov_b32_dpp %32, %21 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %21, %21, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %21, %20, %36 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %20, %20, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32 %20, %32, %35\n\t"
+        "v_mov_b32_dpp %32, %23 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %23, %23, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %23, %22, %36 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %22, %22, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32 %22, %32, %35\n\t"
+        "v_mov_b32_dpp %32, %25 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %25, %25, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %25, %24, %36 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %24, %24, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32 %24, %32, %35\n\t"
+        "v_mov_b32_dpp %32, %27 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %27, %27, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %27, %26, %36 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %26, %26, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32 %26, %32, %35\n\t"
+        "v_mov_b32_dpp %32, %29 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %29, %29, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %29, %28, %36 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %28, %28, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32 %28, %32, %35\n\t"
+        "v_mov_b32_dpp %32, %31 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %31, %31, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %31, %30, %36 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %30, %30, %34 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32 %30, %32, %35\n\t"
+        "s_nop 1"
+        : "+v"(v[0].x), "+v"(v[0].y), "+v"(v[1].x), "+v"(v[1].y), "+v"(v[2].x), "+v"(v[2].y), "+v"(v[3].x), "+v"(v[3].y), "+v"(v[4].x), "+v"(v[4].y), "+v"(v[5].x), "+v"(v[5].y), "+v"(v[6].x), "+v"(v[6].y), "+v"(v[7].x), "+v"(v[7].y), "+v"(v[8].x), "+v"(v[8].y), "+v"(v[9].x), "+v"(v[9].y), "+v"(v[10].x), "+v"(v[10].y), "+v"(v[11].x), "+v"(v[11].y), "+v"(v[12].x), "+v"(v[12].y), "+v"(v[13].x), "+v"(v[13].y), "+v"(v[14].x), "+v"(v[14].y), "+v"(v[15].x), "+v"(v[15].y), "=&v"(t)
+        : "v"(sa), "v"(al), "v"(be), "v"(mbe));
+  }
+}
+
 // decode matrix D_j (true = D * stored) after lane_dft, row-major {d00, d01, d10, d11}
 template <int L, bool INV>
 __host__ __device__ inline void stat_decode(int j, double d[4]) {
@@ -450,7 +621,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     for (int k2 = 0; k2 < 8; ++k2) uc[k2] = uco[g * G::TS + k2];   // in flight under lane_dft
     __builtin_amdgcn_sched_barrier(0);
     MARK(fwd_lane);
-    if (!ABLATE(4)) lane_dft<L, false>(v, g);
+    if (!ABLATE(4)) lane_dft_dpp<L, false>(v, g);
     MARK(untangle);
     // untangle X'[k] = alpha s + beta conj(p), partner bin H - k by DPP
     float2 xs[16];
@@ -641,7 +812,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
       dft<16, true>(v);
 #pragma unroll
       for (int k2 = 1; k2 < 16; ++k2) v[k2] = cmul(v[k2], tw[k2]);
-      lane_dft<L, true>(v, g);
+      lane_dft_dpp<L, true>(v, g);
     }
     MARK(inv_out);
     // y[32 k1 + 2 k2 + {0,1}] = D (R0, R1) / s_C, D = stat_decode<L, true>(g)
@@ -707,6 +878,24 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
 #ifdef STAT_PRIO
   if (wave >= 4) __builtin_amdgcn_s_setprio(STAT_PRIO);   // second-dispatched half wins arbitration
 #endif
+  // experiment hooks: per-phase priority of the second-dispatched half (waves 4-7)
+#ifndef PRIO_INV
+#define PRIO_INV 0
+#endif
+#ifndef PRIO_FWD
+#define PRIO_FWD 0
+#endif
+#ifndef PRIO_MAC
+#define PRIO_MAC 0
+#endif
+  const bool young = wave >= 4;
+  auto setprio = [&](int pr) {
+    if (!young) return;
+    if (pr == 0) __builtin_amdgcn_s_setprio(0);
+    else if (pr == 1) __builtin_amdgcn_s_setprio(1);
+    else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(3);
+  };
   int64_t m = wg_in_grp;
   STAMP(0);
   for (int it = 0; m < n_mtiles || it > 0; ++it, m += gstride) {
@@ -717,6 +906,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     const bool dm = m + gstride < n_mtiles && fwd_active && !ABLATE(16);
     const int sb = 1 + 7 * (it < 7 ? it : 7);       // stamp slots: iterations 0-6, then the latest
     STAMP(sb);
+    if constexpr (PRIO_INV + PRIO_FWD + PRIO_MAC > 0) setprio(PRIO_INV);
     if (st) inverse(other);
     STAMP(sb + 1);
     MARK(store);
@@ -724,10 +914,12 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     if (dm) dma_tile(m + gstride, other);
     STAMP(sb + 2);
     if (!have_f) break;
+    if constexpr (PRIO_INV + PRIO_FWD + PRIO_MAC > 0) setprio(PRIO_FWD);
     if (fwd_active) forward(region, (st ? NST : 0) + (dm ? NDMA : 0));
     STAMP(sb + 3);
     lds_barrier();                                  // Ba: A fragments and scales complete
     STAMP(sb + 4);
+    if constexpr (PRIO_INV + PRIO_FWD + PRIO_MAC > 0) setprio(PRIO_MAC);
     cmac(region);
     STAMP(sb + 5);
     lds_barrier();                                  // Bb: Y image complete

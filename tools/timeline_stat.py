@@ -84,6 +84,11 @@ def run(k, m, b, io, n):
     st, seg = stamps()
     pro = np.median(st[:, 1] - st[:, 0])
     tot = np.median(st[:, 63] - st[:, 0])
+    wv = np.nonzero(buf.view(-1, 64).cpu().numpy()[:, 0])[0] % 8
+    for w in range(8):
+        sel = wv == w
+        if sel.any():
+            print(f"wave {w}        " + " ".join(f"{np.median(seg[sel][:, 1:-1, j]):11.0f}" for j in range(6)))
     print(f"waves {len(st)}, wall {wall:.1f} us, kernel cycles median {tot:.0f} "
           f"-> {tot / wall / 1e3:.2f} GHz implied; prologue {pro:.0f} cycles; first-tile sum "
           f"{np.median(seg[:, 0].sum(axis=1)):.0f}, last-tile sum {np.median(seg[:, -1].sum(axis=1)):.0f}")
