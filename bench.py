@@ -103,6 +103,22 @@ def time_layer(layer, x, steps, warmup, barrier=None):
     return wall, kern
 
 
+def time_spectra(layer, iters=20):
+    """Spectra precompute (rfft(c) + the engines' operand images), ms per call: reported
+    separately, outside the forward's timed region (the cache_cfft=1 convention)."""
+    from bcfft import ops
+    with torch.inference_mode():
+        ops.spectra(layer.c)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(iters):
+            ops.spectra(layer.c)
+        e.record()
+        torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
 def load_traffic(tag):
     """Per-launch HBM bytes from the newest profiles/pmc_traffic_*.json for this workload."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic_*.json")))
@@ -147,7 +163,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--tokens", type=int, default=8192, help="tokens per rank (batch*seq)")
     ap.add_argument("--in-features", type=int, default=4096)
     ap.add_argument("--out-features", type=int, default=4096)
@@ -176,11 +192,50 @@ def main():
     torch.manual_seed(1000 + rank)                           # x ~ N(0,1) per rank shard
     x = torch.randn(n, k, device=dev).to(DT[io])
 
+    # the variant sweep (rank 0, N=1) runs first: real work that also brings the clocks to a
+    # steady state before the contract's timed region
+    variants = []
+    if args.variants and rank == 0 and world == 1:
+        # config 1 (4096², b=64, N=128 fp32), config 2 (4096->11008 b=128 bf16),
+        # the north star in bf16 and on the other engines, and the config-4 sweep b x shape (bf16)
+        vlist = [(4096, 4096, 64, "fp32", 128, "auto"),
+                 (4096, 4096, 128, "bf16", 8192, "auto"),
+                 (4096, 4096, 128, "fp32", 8192, "mfma"),
+                 (4096, 4096, 128, "fp32", 8192, "valu")]
+        for vb in (64, 128, 256):
+            for (vk, vm) in ((4096, 4096), (4096, 11008), (11008, 4096)):
+                if not (vb == 128 and (vk, vm) == (4096, 4096)):
+                    vlist.append((vk, vm, vb, "bf16", 8192, "auto"))
+        for (vk, vm, vb, vio, vn, va) in vlist:
+            os.environ["BCFFT_ALGO"] = va
+            vl = make_layer(vk, vm, vb, vio, False, dev)
+            vx = torch.randn(vn, vk, device=dev).to(DT[vio])
+            vw, vkern = time_layer(vl, vx, max(10, args.steps // 2), 5)
+            os.environ["BCFFT_ALGO"] = algo
+            vbytes = algo_bytes(vn, vk, vm, vb, vio, False)
+            variants.append({"workload": f"{vk}->{vm} b={vb} N={vn} {vio}-io algo={va}",
+                             "engine": resolved_kernel(va, vk, vb)[0],
+                             "ms": round(vkern, 4),
+                             "GTok_elem_s": round(vn * vm / (vkern * 1e-3) / 1e9, 3),
+                             "GB_s": round(vbytes / (vkern * 1e-3) / 1e9, 1),
+                             "frac": round(vbytes / (vkern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+            del vl, vx
     wall, kern = time_layer(layer, x, args.steps, args.warmup, barrier)
     t = torch.tensor([wall, kern], device=dev, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall, kern = float(t[0]), float(t[1])
+
+    # SURVEY.md §8d extras beside the contract's single K-step region: 5 more repeats of K steps
+    # (median and spread of the per-launch kernel time) and the spectra precompute time
+    reps = []
+    for _ in range(5):
+        reps.append(time_layer(layer, x, args.steps, 2, barrier)[1])
+    reps_t = torch.tensor(reps, device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(reps_t, op=dist.ReduceOp.MAX)
+    reps = sorted(float(v) for v in reps_t)
+    spectra_ms = time_spectra(layer)
 
     nbytes = algo_bytes(n, k, m, b, io, bool(args.bias))
     gbs = nbytes / (kern * 1e-3) / 1e9
@@ -207,27 +262,6 @@ def main():
                   "value": round(total_elems / (float(tg[0]) * 1e-3) / 1e9, 3),
                   "note": "forward + RCCL all_gather_into_tensor of all y shards to every rank"}
 
-    variants = []
-    if args.variants and rank == 0 and world == 1:
-        for (vk, vm, vb, vio, vn, va) in [(4096, 4096, 128, "fp32", 8192, "mfma"),
-                                          (4096, 4096, 128, "fp32", 8192, "valu"),
-                                          (4096, 4096, 128, "bf16", 8192, "auto"),
-                                          (4096, 11008, 128, "bf16", 8192, "auto"),
-                                          (11008, 4096, 128, "bf16", 8192, "auto"),
-                                          (4096, 4096, 64, "fp32", 8192, "auto"),
-                                          (4096, 4096, 256, "fp32", 8192, "auto")]:
-            os.environ["BCFFT_ALGO"] = va
-            vl = make_layer(vk, vm, vb, vio, False, dev)
-            vx = torch.randn(vn, vk, device=dev).to(DT[vio])
-            vw, vkern = time_layer(vl, vx, max(10, args.steps // 2), 5)
-            os.environ["BCFFT_ALGO"] = algo
-            vbytes = algo_bytes(vn, vk, vm, vb, vio, False)
-            variants.append({"workload": f"{vk}->{vm} b={vb} N={vn} {vio}-io algo={va}",
-                             "ms": round(vkern, 4),
-                             "GTok_elem_s": round(vn * vm / (vkern * 1e-3) / 1e9, 3),
-                             "GB_s": round(vbytes / (vkern * 1e-3) / 1e9, 1),
-                             "frac": round(vbytes / (vkern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
-            del vl, vx
 
     tag = f"{k}x{m}_b{b}_n{n}_{io}"
     kname = resolved_kernel(algo, k, b)
@@ -261,7 +295,11 @@ def main():
                          "kernel": kname[1], "kernel_ms": round(kern, 5),
                          "algorithmic_bytes_per_launch": nbytes,
                          "fp32_tflops": round(algo_flops(n, k, m, b) / (kern * 1e-3) / 1e12, 2),
-                         "fp32_valu_peak_tflops": FP32_VALU_TFLOPS},
+                         "fp32_valu_peak_tflops": FP32_VALU_TFLOPS,
+                         "kernel_ms_repeats": {"n": len(reps), "steps_each": args.steps,
+                                               "median": round(reps[len(reps) // 2], 5),
+                                               "min": round(reps[0], 5), "max": round(reps[-1], 5)}},
+            "spectra_precompute_ms": round(spectra_ms, 4),
             "cpu_baseline": cpu,
         }
         if gather:

@@ -28,16 +28,19 @@ def t_one(k, m, b, io, algo, n=8192, iters=50):
     us = s.elapsed_time(e) / iters * 1e3
     es = 4 if io == "fp32" else 2
     nbytes = n * k * es + n * m * es + (m // b) * (k // b) * (b // 2 + 1) * 8
-    print(f"{algo:10s} {k}x{m} b{b} {io}: {us:8.1f} us  {nbytes / us / 1e3:7.1f} GB/s  "
+    print(f"{algo:10s} {k}x{m} b{b} {io} N={n}: {us:8.1f} us  {nbytes / us / 1e3:7.1f} GB/s  "
           f"{nbytes / us / 1e3 / 8000:.3f} of 8 TB/s", flush=True)
 
 
 if __name__ == "__main__":
-    shapes = [(4096, 4096, 128, "fp32"), (4096, 4096, 128, "bf16"), (4096, 11008, 128, "bf16"),
-              (4096, 4096, 64, "fp32")]
-    for sh in shapes:
-        for algo in sys.argv[1:] or ["stationary", "mfma", "valu"]:
+    shapes = [(4096, 4096, 128, "fp32", 8192), (4096, 4096, 128, "bf16", 8192), (4096, 11008, 128, "bf16", 8192),
+              (4096, 4096, 64, "fp32", 8192)]
+    algos = [a for a in sys.argv[1:] if not a.startswith("--")] or ["stationary", "mfma", "valu"]
+    if "--smalln" in sys.argv:                      # AUTO's small-N crossover
+        shapes = [(4096, 4096, b, io, n) for b in (64, 128) for io in ("fp32",) for n in (16, 64, 128, 256, 512, 1024, 2048)]
+    for k, m, b, io, n in shapes:
+        for algo in algos:
             try:
-                t_one(*sh, algo)
+                t_one(k, m, b, io, algo, n=n)
             except RuntimeError as ex:
-                print(algo, sh, "n/a:", str(ex)[:80])
+                print(algo, (k, m, b, io, n), "n/a:", str(ex)[:80])
