@@ -875,27 +875,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
   // (Measured alternatives: issuing the stores and DMA inside the forward, after its x reads,
   // and running inverse / forward in opposite orders on SIMD mates were both slower.)
   const bool fwd_active = wave < NWF, inv_active = wave < NWI;
-#ifdef STAT_PRIO
-  if (wave >= 4) __builtin_amdgcn_s_setprio(STAT_PRIO);   // second-dispatched half wins arbitration
-#endif
-  // experiment hooks: per-phase priority of the second-dispatched half (waves 4-7)
-#ifndef PRIO_INV
-#define PRIO_INV 0
-#endif
-#ifndef PRIO_FWD
-#define PRIO_FWD 0
-#endif
-#ifndef PRIO_MAC
-#define PRIO_MAC 0
-#endif
-  const bool young = wave >= 4;
-  auto setprio = [&](int pr) {
-    if (!young) return;
-    if (pr == 0) __builtin_amdgcn_s_setprio(0);
-    else if (pr == 1) __builtin_amdgcn_s_setprio(1);
-    else if (pr == 2) __builtin_amdgcn_s_setprio(2);
-    else __builtin_amdgcn_s_setprio(3);
-  };
   int64_t m = wg_in_grp;
   STAMP(0);
   for (int it = 0; m < n_mtiles || it > 0; ++it, m += gstride) {
@@ -906,7 +885,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     const bool dm = m + gstride < n_mtiles && fwd_active && !ABLATE(16);
     const int sb = 1 + 7 * (it < 7 ? it : 7);       // stamp slots: iterations 0-6, then the latest
     STAMP(sb);
-    if constexpr (PRIO_INV + PRIO_FWD + PRIO_MAC > 0) setprio(PRIO_INV);
     if (st) inverse(other);
     STAMP(sb + 1);
     MARK(store);
@@ -914,12 +892,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     if (dm) dma_tile(m + gstride, other);
     STAMP(sb + 2);
     if (!have_f) break;
-    if constexpr (PRIO_INV + PRIO_FWD + PRIO_MAC > 0) setprio(PRIO_FWD);
     if (fwd_active) forward(region, (st ? NST : 0) + (dm ? NDMA : 0));
     STAMP(sb + 3);
     lds_barrier();                                  // Ba: A fragments and scales complete
     STAMP(sb + 4);
-    if constexpr (PRIO_INV + PRIO_FWD + PRIO_MAC > 0) setprio(PRIO_MAC);
     cmac(region);
     STAMP(sb + 5);
     lds_barrier();                                  // Bb: Y image complete

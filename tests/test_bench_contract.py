@@ -1,0 +1,45 @@
+"""bench.py keeps the driver's contract: the SURVEY.md §8d byte figures, the engine each BCFFT_ALGO
+resolves to, and (GPU) one JSON line with the required keys, roofline and cpu_baseline."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_algorithmic_bytes_match_survey():
+    assert bench.algo_bytes(8192, 4096, 4096, 128, "fp32", False) == 268_967_936
+    assert bench.algo_bytes(8192, 4096, 4096, 128, "bf16", False) == 134_750_208
+
+
+def test_engine_resolution_mirrors_auto_rule():
+    assert bench.resolved_kernel("auto", 4096, 128)[1] == "bc_forward_stat_kernel"
+    assert bench.resolved_kernel("auto", 4096, 64)[1] == "bc_forward_stat_kernel"
+    assert bench.resolved_kernel("auto", 2048, 64)[1] == "bc_forward_stat_kernel"
+    assert bench.resolved_kernel("auto", 11008, 128)[1] == "bc_forward_mfma_kernel"
+    assert bench.resolved_kernel("auto", 4096, 256)[1] == "bc_forward_valu_kernel"
+    assert bench.resolved_kernel("valu", 4096, 128)[1] == "bc_forward_valu_kernel"
+
+
+@pytest.mark.gpu
+def test_bench_prints_one_contract_line():
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "2",
+                          "--variants", "0", "--cpu-budget", "0"], capture_output=True, text=True,
+                         timeout=300, check=True).stdout
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    d = json.loads(lines[0])
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert key in d, key
+    assert d["n_gpus"] == 1 and d["steps"] == 5 and d["warmup"] == 2
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    assert r["kernel"] == "bc_forward_stat_kernel"
