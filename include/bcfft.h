@@ -100,6 +100,19 @@ int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_feat
                        int out_features, int block_size, const void* spectra, const void* bias,
                        int bias_dtype, void* y, int y_dtype, int algo, void* stream);
 
+/* Fused gate/up projections + SwiGLU of a LLaMA MLP (the reference MLP
+ * computes down(act(gate(x)) * up(x)) with gate/up BC-patched by patch_llama_fft.py:343-394;
+ * act = SiLU): h = silu(BC_gate(x)) * BC_up(x) in ONE launch, without writing gate(x) and up(x)
+ * to memory. spectra_gu = bcfft_spectra of the interleaved weight c_gu of shape
+ * (32 * ceil(gate_blocks / 16), in_blocks, b): group g's 32 blocks are gate blocks [16g, 16g+16)
+ * then up blocks [16g, 16g+16), zero past the last gate block (bcfft.ops.glu_weights builds it).
+ *   x: (n_tokens, in_features), h: (n_tokens, gate_features), both x_dtype, 16-B aligned
+ * Stationary geometries only (b = 128 with K = 4096; b = 64 with K in {2048, 4096}), else
+ * BCFFT_ERR_BLOCK; no bias (LLaMA's gate/up have none). Numerics follow torch on the reference's
+ * tensors: gate and up rounded to x_dtype, silu(gate) rounded, the product rounded. */
+int bcfft_forward_glu(const void* x, int x_dtype, int64_t n_tokens, int in_features, int gate_features,
+                      int block_size, const void* spectra_gu, void* h, void* stream);
+
 /* Single circulant matvec y = C(c) x, C[i,j] = c[(i-j) mod n], any n >= 1.
  * Replaces fft_utils.circulant_matvec_fft (fft_utils.py:3-34); c, x, y share `dtype`.
  * Direct O(n^2) evaluation accumulated in fp64 (this entry point serves validation-sized

@@ -40,6 +40,48 @@ def spectra(c: torch.Tensor, transpose_conj: bool = False) -> torch.Tensor:
     return out
 
 
+def glu_weights(c_gate: torch.Tensor, c_up: torch.Tensor) -> torch.Tensor:
+    """Interleave gate/up circulant columns (nO, nI, b) into the (32 G, nI, b) weight of
+    bcfft_forward_glu, G = ceil(nO / 16): group g = gate blocks [16g, 16g+16) then up blocks
+    [16g, 16g+16), zero blocks past nO. Pure indexing (any device)."""
+    if c_gate.shape != c_up.shape or c_gate.dim() != 3:
+        raise ValueError("gate and up weights must both be (out_blocks, in_blocks, block_size)")
+    n_out, n_in, b = c_gate.shape
+    groups = -(-n_out // 16)
+    flat = c_gate.new_zeros(groups, 2, 16, n_in, b)
+    gpad = torch.zeros(groups * 16, n_in, b, dtype=c_gate.dtype, device=c_gate.device)
+    upad = torch.zeros_like(gpad)
+    gpad[:n_out] = c_gate.detach()
+    upad[:n_out] = c_up.detach()
+    flat[:, 0] = gpad.view(groups, 16, n_in, b)
+    flat[:, 1] = upad.view(groups, 16, n_in, b)
+    return flat.reshape(groups * 32, n_in, b)
+
+
+def forward_glu(x2d: torch.Tensor, spec_gu: torch.Tensor, block_size: int, gate_features: int) -> torch.Tensor:
+    """h = silu(BC_gate(x2d)) * BC_up(x2d) in one launch (bcfft_forward_glu); spec_gu =
+    spectra(glu_weights(c_gate, c_up)). h has x2d's dtype."""
+    _lib.require_device(x2d, "bcfft.forward_glu")
+    n, k = x2d.shape
+    x2d = x2d.contiguous()
+    if x2d.data_ptr() % 16:
+        x2d = x2d.clone()
+    h = torch.empty((n, gate_features), dtype=x2d.dtype, device=x2d.device)
+    if n == 0:
+        return h
+    lib = _lib.load()
+    _lib.check(lib.bcfft_forward_glu(x2d.data_ptr(), _lib.dtype_code(x2d.dtype), n, k, gate_features,
+                                     block_size, spec_gu.data_ptr(), h.data_ptr(),
+                                     _lib.stream_handle(x2d.device)), "bcfft_forward_glu")
+    return h
+
+
+def glu_eligible(in_features: int, block_size: int) -> bool:
+    """Geometries the fused gate/up kernel serves (the stationary ones, include/bcfft.h)."""
+    n_in = in_features // block_size
+    return (block_size == 128 and n_in == 32) or (block_size == 64 and n_in in (32, 64))
+
+
 def default_algo() -> str:
     """BCFFT_ALGO env var: auto (default) | stationary | mfma | valu."""
     import os

@@ -43,6 +43,17 @@ __device__ __forceinline__ uint32_t pack16(float a, float b) {
     return __builtin_bit_cast(uint32_t, h);
   }
 }
+// packed 16-bit pair (low = first) -> two floats (exact)
+template <int DT>
+__device__ __forceinline__ float2 unpack16(uint32_t p) {
+  if constexpr (DT == BCFFT_BF16) return make_float2(__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u));
+  else return make_float2(f16_to_f32(p & 0xffffu), f16_to_f32(p >> 16));
+}
+// torch's SiLU in fp32, x * sigmoid(x) = x / (1 + e^-x): hardware exp and reciprocal (~1 ulp each;
+// e^-x -> inf gives -0 / NaN as torch does for x -> -inf)
+__device__ __forceinline__ float silu(float x) {
+  return x * __builtin_amdgcn_rcpf(1.f + __expf(-x));
+}
 // round a pair to DT and back: the packed pair's halves widened (exact)
 template <int DT>
 __device__ __forceinline__ float2 round_pair(float a, float b) {
@@ -420,6 +431,10 @@ __host__ __device__ inline SpecLayout spec_layout(int n_out, int n_in, int b) {
 // geometry / dtype combination has no instantiation
 bool launch_forward_stat(int b, int n_in, int xdt, bool yf32, const void* x, int64_t n, int n_out,
                          const void* spec, const void* bias, int bias_dt, void* y, hipStream_t s);
+// fused gate/up + SwiGLU: h = silu(x Cg) * (x Cu); spec holds ceil(n_gate/16) groups of 32
+// interleaved blocks (16 gate, 16 up). false if the geometry is not stationary-eligible.
+bool launch_forward_glu(int b, int n_in, int xdt, const void* x, int64_t n, int n_gate, const void* spec,
+                        void* h, hipStream_t s);
 void launch_stat_image(int b, int n_out, int n_in, void* spec, hipStream_t s);
 
 }  // namespace bcfft

@@ -681,6 +681,22 @@ int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_feat
   return record_launch();
 }
 
+int bcfft_forward_glu(const void* x, int x_dtype, int64_t n_tokens, int in_features, int gate_features,
+                      int block_size, const void* spectra_gu, void* h, void* stream) {
+  if (!valid_block(block_size)) return BCFFT_ERR_BLOCK;
+  if (n_tokens < 0 || in_features <= 0 || gate_features <= 0 || in_features % block_size ||
+      gate_features % block_size)
+    return BCFFT_ERR_SHAPE;
+  if (!valid_dt(x_dtype)) return BCFFT_ERR_DTYPE;
+  const int n_in = in_features / block_size, n_gate = gate_features / block_size;
+  if (!bcfft::stat_eligible(n_in, block_size)) return BCFFT_ERR_BLOCK;
+  if (n_tokens == 0) return BCFFT_OK;
+  if (!x || !h || !spectra_gu) return BCFFT_ERR_ARG;
+  if (!aligned16(x) || !aligned16(h) || !aligned16(spectra_gu)) return BCFFT_ERR_ALIGN;
+  bcfft::launch_forward_glu(block_size, n_in, x_dtype, x, n_tokens, n_gate, spectra_gu, h, (hipStream_t)stream);
+  return record_launch();
+}
+
 int bcfft_forward(const void* x, int x_dtype, int64_t n_tokens, int in_features,
                   int out_features, int block_size, const void* spectra, const void* bias,
                   int bias_dtype, void* y, int y_dtype, void* stream) {

@@ -353,7 +353,7 @@ __device__ __forceinline__ int swz_x(int r) {
   return ES == 4 ? (L == 4 ? 2 * (r & 7) : (r & 15)) : (r & 7);
 }
 
-template <int B, int KS, int XT, bool YF32>
+template <int B, int KS, int XT, bool YF32, bool GLU>
 __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_out, const uint32_t* __restrict__ stat,
     const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
@@ -387,7 +387,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // 1-D grid, one workgroup per CU: workgroup i serves output group i % groups and, with the
   // other workgroups of that group, strides over the M-tiles
-  const int n_groups = (n_out + G::NOG - 1) / G::NOG;
+  // GLU: n_out counts gate blocks; group g holds gate blocks [16g, 16g+16) and the matching up
+  // blocks as its 32 output blocks, and h = silu(gate) * up has n_out blocks
+  constexpr int OPG = GLU ? G::NOG / 2 : G::NOG;   // output blocks stored per group
+  const int n_groups = (n_out + OPG - 1) / OPG;
   const int grp_o = blockIdx.x % n_groups;         // output group
   const int wg_in_grp = blockIdx.x / n_groups;
   const int64_t M = (int64_t)n_out * B;
@@ -525,6 +528,26 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     else
       return gi;
   };
+  // output row R = 32 t + o (token t of the tile, block o of the group) <-> (slot, row r). Plain:
+  // slot R / RPWI. GLU at b = 128: slot 2t + ((o >> 3) & 1) holds o in 8 half + [0, 8) as
+  // r = o & 7 and o + 16 as r + 8, so a wave owns both the gate and the up row of its outputs
+  // (at b = 64 a slot is a whole token already: gate r < 16, up r + 16)
+  auto slot_of_row = [](int R, int& r) {
+    if constexpr (GLU && RPWI == 16) {
+      const int o = R & 31;
+      r = (o & 7) + 8 * (o >> 4);
+      return 2 * (R >> 5) + ((o >> 3) & 1);
+    } else {
+      r = R % RPWI;
+      return R / RPWI;
+    }
+  };
+  auto row_of_slot = [](int w, int r) {
+    if constexpr (GLU && RPWI == 16)
+      return 32 * (w >> 1) + 8 * (w & 1) + (r & 7) + 16 * (r >> 3);
+    else
+      return w * RPWI + r;
+  };
   // y staging: 16-B piece pc of row r goes to unit pc of row r ^ hmap(pc) (same slot), which
   // spreads one store instruction's pieces over the banks; hmap is linear in the bits of pc
   constexpr int NQL = 32 * ESY / 16;               // 16-B pieces of y per lane
@@ -576,13 +599,65 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     }
   };
 
+  // GLU epilogue: the wave's RPWI/2 h rows, h = silu(g) * u from its staged gate row r and up
+  // row r + RPWI/2, with torch's roundings for 16-bit tensors (silu(g) rounded to the dtype,
+  // then the product rounded). Same global order and 1 KiB instructions as store_tile.
+  auto glu_store = [&](int64_t mt, const char* regn) {
+    if constexpr (GLU) {
+      if (wave >= NWI) return;
+      constexpr int NSTG = NST / 2;
+      const int64_t stok0 = mt * TT;
+      const int64_t ntok = n_tokens - stok0 < TT ? n_tokens - stok0 : TT;
+      const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+          (char*)yv + stok0 * M * ESY, 0, (int)(ntok * M * ESY), 0x00020000);
+      const int slane = opaque(lane);
+      const int pc = slane & (NPR - 1);
+      const int r0 = (int)((unsigned)slane / NPR);
+      const int src0 = wave * SLOT + yunit(pc, r0 ^ hmap(pc));
+      const int rho0 = row_of_slot(wave, r0);       // gate row: token rho >> 5, block rho & 15
+      const int j0 = rho0 & 15;
+      const int yoff0 = (int)((((int64_t)(rho0 >> 5) * M) + (int64_t)(grp_o * OPG + j0) * B) * ESY) + 16 * pc;
+      const int nvalid = n_out - grp_o * OPG;
+      uint4 gq[NSTG], uq[NSTG];
+#pragma unroll
+      for (int q = 0; q < NSTG; ++q) {
+        gq[q] = *reinterpret_cast<const uint4*>(regn + (src0 ^ (16 * q * RPI)));
+        uq[q] = *reinterpret_cast<const uint4*>(regn + (src0 ^ (16 * q * RPI) ^ (16 * RPWI / 2)));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < NSTG; ++q) {
+        uint4 hq;
+        if constexpr (Y32) {
+          const float4 gv = __builtin_bit_cast(float4, gq[q]), uv = __builtin_bit_cast(float4, uq[q]);
+          hq = __builtin_bit_cast(uint4, make_float4(silu(gv.x) * uv.x, silu(gv.y) * uv.y,
+                                                     silu(gv.z) * uv.z, silu(gv.w) * uv.w));
+        } else {
+          const uint32_t* gw = reinterpret_cast<const uint32_t*>(&gq[q]);
+          const uint32_t* uw = reinterpret_cast<const uint32_t*>(&uq[q]);
+          uint32_t hw[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float2 g2 = unpack16<XT>(gw[e]), u2 = unpack16<XT>(uw[e]);
+            const float2 s2 = round_pair<XT>(silu(g2.x), silu(g2.y));
+            hw[e] = pack16<XT>(s2.x * u2.x, s2.y * u2.y);
+          }
+          hq = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+        }
+        const int yoff = nvalid >= OPG || j0 + q * RPI < nvalid ? yoff0 + q * RPI * B * ESY : 0x7fff0000;
+        if (!ABLATE(2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hq), yrs, yoff, 0, 0);
+      }
+    }
+  };
+
   // ---- forward of one M-tile (wave w < NWF, slot w): x rows -> real-FFT bins X' -> scaled
   // fp16 hi/lo A fragments in place. All RPWF rows of the wave are one token's K-step(s): the
   // wave's own max |X'| sets the scale s = 2^(15 - E) (max < 2^E), exponent posted to wsc[w].
   auto forward = [&](char* region, int younger) {
     // this wave's x rows landed: everything but the `younger` VMEM ops issued after them
-    if (younger == NST + NDMA) wait_vmcnt<NST + NDMA>();
-    else if (younger == NST) wait_vmcnt<NST>();
+    constexpr int NSTW = GLU ? NST / 2 : NST;
+    if (younger == NSTW + NDMA) wait_vmcnt<NSTW + NDMA>();
+    else if (younger == NSTW) wait_vmcnt<NSTW>();
     else if (younger == NDMA) wait_vmcnt<NDMA>();
     else wait_vmcnt<0>();
     MARK(fwd_read);
@@ -757,8 +832,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
       const int p = (wave * BW) / 2 + fp;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        const int R = yt * G::NOG + nt * 16 + (mlane & 15);
-        *reinterpret_cast<float4*>(region + (R / RPWI) * SLOT + yunit(p, R % RPWI)) =
+        int yr;
+        const int ys = slot_of_row(yt * G::NOG + nt * 16 + (mlane & 15), yr);
+        *reinterpret_cast<float4*>(region + ys * SLOT + yunit(p, yr)) =
             make_float4(ybuf[0][nt].x, ybuf[0][nt].y, ybuf[1][nt].x, ybuf[1][nt].y);
       }
     }
@@ -772,7 +848,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     const int gi = (int)((unsigned)(ptid & 63) / L), g = ptid & (L - 1);
     const int k1 = k1_of<L>(g);
     const int r = inv_row(gi);
-    const int R = wave * RPWI + r;                  // token R >> 5, output block R & 31
+    const int R = row_of_slot(wave, r);             // token R >> 5, output block R & 31
     const int inv_o = R & (G::NOG - 1);
     char* slot = region + wave * SLOT;
     // Y[k], k = g + L n2: unit (g >> 1) + (L/2) n2, half g & 1. Y[H-k] = (H-L-L n2) + (L-g):
@@ -883,16 +959,20 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     const bool have_f = m < n_mtiles;
     const bool st = it > 0 && inv_active;
     const bool dm = m + gstride < n_mtiles && fwd_active && !ABLATE(16);
+    constexpr int NSTV = GLU ? NST / 2 : NST;       // VMEM stores issued per wave per tile
     const int sb = 1 + 7 * (it < 7 ? it : 7);       // stamp slots: iterations 0-6, then the latest
     STAMP(sb);
     if (st) inverse(other);
     STAMP(sb + 1);
     MARK(store);
-    if (st) store_tile(m - gstride, other);
+    if (st) {
+      if constexpr (GLU) glu_store(m - gstride, other);
+      else store_tile(m - gstride, other);
+    }
     if (dm) dma_tile(m + gstride, other);
     STAMP(sb + 2);
     if (!have_f) break;
-    if (fwd_active) forward(region, (st ? NST : 0) + (dm ? NDMA : 0));
+    if (fwd_active) forward(region, (st ? NSTV : 0) + (dm ? NDMA : 0));
     STAMP(sb + 3);
     lds_barrier();                                  // Ba: A fragments and scales complete
     STAMP(sb + 4);
@@ -987,11 +1067,12 @@ int cu_count() {
   return g_cu_count;
 }
 
-template <int B, int KS, int XT, bool YF32>
+template <int B, int KS, int XT, bool YF32, bool GLU = false>
 void launch_stat(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt,
                  void* y, hipStream_t s) {
-  const bcfft::SpecLayout sl = bcfft::spec_layout(n_out, 16 * KS, B);
-  const int groups = sl.stat_groups;
+  // GLU: n_out = gate blocks; the spectra hold groups x 32 interleaved gate/up blocks
+  const int groups = GLU ? (n_out + 15) / 16 : (n_out + 31) / 32;
+  const bcfft::SpecLayout sl = bcfft::spec_layout(GLU ? 32 * groups : n_out, 16 * KS, B);
   // one workgroup per CU (1-D grid, group = index % groups): every group gets cus/groups
   // workgroups, rounded either way, instead of a whole-XCD multiple (11 groups: 253 vs 176)
   const int64_t n_mtiles = (n + 3) / 4;
@@ -999,7 +1080,7 @@ void launch_stat(const void* x, int64_t n, int n_out, const void* spec, const vo
   if (total > groups * n_mtiles) total = groups * n_mtiles;
   if (total < groups) total = groups;
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
-  hipLaunchKernelGGL((bcfft::bc_forward_stat_kernel<B, KS, XT, YF32>), dim3((unsigned)total), dim3(512), 0, s,
+  hipLaunchKernelGGL((bcfft::bc_forward_stat_kernel<B, KS, XT, YF32, GLU>), dim3((unsigned)total), dim3(512), 0, s,
                      x, n, n_out, stat, bias, bias_dt, y);
 }
 
@@ -1013,9 +1094,24 @@ bool launch_stat_dt(int xdt, bool yf32, const void* x, int64_t n, int n_out, con
   else launch_stat<B, KS, BCFFT_BF16, false>(x, n, n_out, spec, bias, bias_dt, y, s);
   return true;
 }
+template <int B, int KS>
+void launch_glu_dt(int xdt, const void* x, int64_t n, int n_gate, const void* spec, void* h, hipStream_t s) {
+  if (xdt == BCFFT_F32) launch_stat<B, KS, BCFFT_F32, true, true>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
+  else if (xdt == BCFFT_F16) launch_stat<B, KS, BCFFT_F16, false, true>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
+  else launch_stat<B, KS, BCFFT_BF16, false, true>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
+}
 }  // namespace
 
 namespace bcfft {
+bool launch_forward_glu(int b, int n_in, int xdt, const void* x, int64_t n, int n_gate, const void* spec,
+                        void* h, hipStream_t s) {
+  if (!stat_eligible(n_in, b)) return false;
+  if (b == 128) launch_glu_dt<128, 2>(xdt, x, n, n_gate, spec, h, s);
+  else if (n_in == 64) launch_glu_dt<64, 4>(xdt, x, n, n_gate, spec, h, s);
+  else launch_glu_dt<64, 2>(xdt, x, n, n_gate, spec, h, s);
+  return true;
+}
+
 bool launch_forward_stat(int b, int n_in, int xdt, bool yf32, const void* x, int64_t n, int n_out,
                          const void* spec, const void* bias, int bias_dt, void* y, hipStream_t s) {
   if (!stat_eligible(n_in, b)) return false;

@@ -328,6 +328,76 @@ def patch_linear_with_block_circulant(model, *, num_layers_to_patch: int = NUM_L
     _patch(model, layer_indices, block_size, tuple(targets))
 
 
+class BCFusedGateUp(nn.Module):
+    """act(gate(x)) * up(x) of a BC-patched LLaMA MLP in ONE launch (bcfft_forward_glu,
+    include/bcfft.h): the gate and up projections share x's forward FFT in
+    each workgroup and neither gate(x) nor up(x) is written to memory.
+
+    Holds plain references to the two BlockCirculantLinear modules (their parameters and
+    state_dict keys stay where they are). Uses the two modules + torch SiLU instead when the
+    fused kernel does not apply: a bias, autograd recording, or a non-stationary geometry."""
+
+    def __init__(self, gate: BlockCirculantLinear, up: BlockCirculantLinear):
+        super().__init__()
+        if (gate.in_features, gate.out_features, gate.block_size) != (up.in_features, up.out_features, up.block_size):
+            raise ValueError("gate and up projections must have the same shape and block_size")
+        object.__setattr__(self, "_gate", gate)          # not submodules: no duplicate parameters
+        object.__setattr__(self, "_up", up)
+        self._spec = None
+        self._key = None
+
+    def _fused_ok(self, x: torch.Tensor) -> bool:
+        g, u = self._gate, self._up
+        grad = torch.is_grad_enabled() and (g.c.requires_grad or u.c.requires_grad or x.requires_grad)
+        return (g.bias is None and u.bias is None and not grad and x.is_cuda
+                and _ops.glu_eligible(g.in_features, g.block_size))
+
+    def _spectra(self) -> torch.Tensor:
+        g, u = self._gate.c, self._up.c
+        key = (g.device, g.data_ptr(), g._version, u.data_ptr(), u._version, g.dtype)
+        if key != self._key:
+            self._spec = _ops.spectra(_ops.glu_weights(g, u))
+            self._key = key
+        return self._spec
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not self._fused_ok(x):
+            return torch.nn.functional.silu(self._gate(x)) * self._up(x)
+        shape = x.shape
+        x2d = x.reshape(-1, shape[-1])
+        h = _ops.forward_glu(x2d, self._spectra(), self._gate.block_size, self._gate.out_features)
+        return h.view(*shape[:-1], self._gate.out_features)
+
+
+def _fused_mlp_forward(self, x):
+    return self.down_proj(self._bc_gate_up(x))
+
+
+def fuse_mlp_gate_up(model) -> int:
+    """Route each decoder MLP whose gate_proj and up_proj are BlockCirculantLinear (same shape,
+    act = SiLU, as patch_mlp_with_block_circulant leaves them) through BCFusedGateUp: its
+    forward becomes down_proj(silu(gate(x)) * up(x)) with the fused launch. Parameters and
+    state_dict are unchanged. Returns the number of MLPs rewired."""
+    import types
+    n = 0
+    for layer in model.model.layers:
+        mlp = getattr(layer, "mlp", None)
+        if mlp is None:
+            continue
+        g, u = getattr(mlp, "gate_proj", None), getattr(mlp, "up_proj", None)
+        if not (isinstance(g, BlockCirculantLinear) and isinstance(u, BlockCirculantLinear)):
+            continue
+        act = getattr(mlp, "act_fn", None)          # nn.SiLU, or transformers' SiLUActivation
+        if not (isinstance(act, nn.SiLU) or type(act).__name__ == "SiLUActivation"):
+            continue
+        if (g.in_features, g.out_features, g.block_size) != (u.in_features, u.out_features, u.block_size):
+            continue
+        object.__setattr__(mlp, "_bc_gate_up", BCFusedGateUp(g, u))
+        mlp.forward = types.MethodType(_fused_mlp_forward, mlp)
+        n += 1
+    return n
+
+
 def main():
     """patch_llama_fft.py:396-419 — load LLaMA from MODEL_PATH, patch, run a shape check."""
     from transformers import AutoModelForCausalLM

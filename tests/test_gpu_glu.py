@@ -1,0 +1,125 @@
+"""GPU parity of the fused gate/up + SwiGLU launch (bcfft_forward_glu)
+against the CPU oracle: h = silu(BC_gate(x)) * BC_up(x), the LLaMA MLP's inner product of
+patch_mlp_with_block_circulant's gate/up projections (patch_llama_fft.py:343-394).
+
+The oracle follows torch on the reference's tensors: gate(x) and up(x) rounded to x's dtype
+(the BC forward's .to(x.dtype), patch_llama_fft.py:266), SiLU computed in fp32 and rounded,
+the product rounded. The weights are the stationary kernel's fp16 (~3e-4 per output), and SiLU
+and the product carry that error along, so fp32 outputs are checked at 1e-3 relative Frobenius
+and 16-bit outputs within ~2 output ulp plus 2e-3 (the weight error SiLU can amplify) per
+element, plus the norm bound."""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import rel_err
+from oracle import bc_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TDT = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16}
+ODT = {"float32": O.F32, "float16": O.F16, "bfloat16": O.BF16}
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    import bcfft
+    bcfft.load()
+    return torch.device("cuda:0")
+
+
+def _silu(a):
+    return a / (1.0 + np.exp(-a.astype(np.float64)))
+
+
+def oracle_glu(x, cg, cu, xdt):
+    xr = O.round_to(x, ODT[xdt])
+    g = O.bc_forward(xr, cg, x_dtype=ODT[xdt])         # rounded to x dtype (:266)
+    u = O.bc_forward(xr, cu, x_dtype=ODT[xdt])
+    s = O.round_to(_silu(g).astype(np.float32), ODT[xdt])
+    return O.round_to((s.astype(np.float64) * u).astype(np.float32), ODT[xdt])
+
+
+def _check(h, ref, xdt):
+    g = h.detach().float().cpu().numpy()
+    assert g.shape == ref.shape and np.isfinite(g).all()
+    e = rel_err(g, ref)
+    if xdt == "float32":
+        assert e < 1e-3, f"rel err {e:.3e}"
+    else:
+        ulp = 2.0 ** -7 if xdt == "bfloat16" else 2.0 ** -10
+        rms = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
+        # 2 output ulp of rounding plus the weights' ~3e-4 carried through SiLU, whose relative
+        # sensitivity |1 + g (1 - sigmoid(g))| reaches ~|g| for negative g: 2e-3 per element
+        bad = np.abs(g - ref) > (2 * ulp + 2e-3) * np.abs(ref) + 2 * ulp * rms
+        assert not bad.any(), f"{int(bad.sum())} elements beyond ~2 ulp"
+        assert e < 4e-3, e
+    return e
+
+
+CASES = [
+    # (K, M_gate, b, N, dtype)
+    (4096, 11008, 128, 37, "bfloat16"),   # LLaMA-7B gate/up shape: 86 blocks -> 6 groups, last partial
+    (4096, 4096, 128, 9, "float32"),
+    (4096, 4096, 128, 64, "float16"),
+    (4096, 11008, 64, 23, "bfloat16"),    # b = 64, 4 K-steps, 172 blocks -> 11 groups
+    (2048, 5632, 64, 5, "float32"),       # b = 64, 2 K-steps, 88 blocks
+    (4096, 2048, 128, 1, "float32"),      # one token, one group
+]
+
+
+@pytest.mark.parametrize("k,m,b,n,xdt", CASES)
+def test_glu_vs_oracle(dev, k, m, b, n, xdt):
+    from bcfft import ops
+    rng = np.random.default_rng(k + m + b + n)
+    cg = (rng.standard_normal((m // b, k // b, b)) * 0.01).astype(np.float32)
+    cu = (rng.standard_normal((m // b, k // b, b)) * 0.01).astype(np.float32)
+    x = rng.standard_normal((n, k)).astype(np.float32)
+    spec = ops.spectra(ops.glu_weights(torch.from_numpy(cg).to(dev), torch.from_numpy(cu).to(dev)))
+    h = ops.forward_glu(torch.from_numpy(x).to(dev).to(TDT[xdt]), spec, b, m)
+    torch.cuda.synchronize()
+    assert h.dtype == TDT[xdt] and h.shape == (n, m)
+    _check(h, oracle_glu(x, cg, cu, xdt), xdt)
+
+
+def test_glu_equals_unfused_composition(dev):
+    """The fused launch against the two stationary launches + torch SiLU and product."""
+    from bcfft import ops
+    torch.manual_seed(3)
+    k, m, b = 4096, 11008, 128
+    cg = torch.randn(m // b, k // b, b, device=dev) * 0.01
+    cu = torch.randn(m // b, k // b, b, device=dev) * 0.01
+    x = torch.randn(301, k, device=dev).to(torch.bfloat16)
+    h = ops.forward_glu(x, ops.spectra(ops.glu_weights(cg, cu)), b, m)
+    ref = torch.nn.functional.silu(ops.forward(x, ops.spectra(cg), None, b, m)) * ops.forward(x, ops.spectra(cu), None, b, m)
+    d = (h.float() - ref.float()).abs()
+    assert (d <= 2 * 2.0 ** -7 * ref.float().abs() + 1e-6).float().mean().item() > 0.999
+    assert ((h.float() - ref.float()).norm() / ref.float().norm()).item() < 4e-3
+
+
+def test_glu_rejects_ineligible_geometry(dev):
+    from bcfft import ops
+    cg = torch.zeros(4, 4, 128, device=dev)
+    spec = ops.spectra(ops.glu_weights(cg, cg))
+    with pytest.raises(RuntimeError, match="block_size"):
+        ops.forward_glu(torch.zeros(3, 512, device=dev), spec, 128, 512)
+
+
+def test_fused_mlp_module_matches_unfused(dev):
+    """BCFusedGateUp / fuse_mlp_gate_up on a one-layer LLaMA patched with b = 64 blocks."""
+    transformers = pytest.importorskip("transformers")
+    import patch_llama_fft as P
+    torch.manual_seed(0)
+    cfg = transformers.LlamaConfig(hidden_size=2048, intermediate_size=5632, num_hidden_layers=1,
+                                   num_attention_heads=16, num_key_value_heads=16, vocab_size=256,
+                                   max_position_embeddings=64)
+    model = transformers.LlamaForCausalLM(cfg).eval()
+    P.patch_mlp_with_block_circulant(model, num_layers_to_patch=1, block_size=64)
+    model = model.to(dev)
+    ids = torch.randint(0, 256, (2, 16), device=dev)
+    with torch.no_grad():
+        ref = model(input_ids=ids).logits.float()
+        assert P.fuse_mlp_gate_up(model) == 1
+        out = model(input_ids=ids).logits.float()
+    assert ((out - ref).norm() / ref.norm()).item() < 1e-3

@@ -120,3 +120,30 @@ def test_forward_refuses_cpu(plf):
         m(torch.zeros(2, 128))
     with pytest.raises(ValueError, match="Unsupported input dim"):
         m(torch.zeros(128))
+
+
+def test_glu_weights_interleave_groups():
+    """bcfft_forward_glu's weight layout: group g = gate blocks [16g, 16g+16), up blocks."""
+    from bcfft import ops
+    g = torch.randn(40, 3, 8)
+    u = torch.randn(40, 3, 8)
+    w = ops.glu_weights(g, u)
+    assert w.shape == (96, 3, 8)
+    for grp in range(3):
+        n = min(16, 40 - 16 * grp)
+        assert torch.equal(w[32 * grp:32 * grp + n], g[16 * grp:16 * grp + n])
+        assert torch.equal(w[32 * grp + 16:32 * grp + 16 + n], u[16 * grp:16 * grp + n])
+        assert (w[32 * grp + n:32 * grp + 16] == 0).all() and (w[32 * grp + 16 + n:32 * grp + 32] == 0).all()
+
+
+def test_fuse_mlp_gate_up_rewires_without_new_parameters():
+    transformers = pytest.importorskip("transformers")
+    import patch_llama_fft as P
+    cfg = transformers.LlamaConfig(hidden_size=256, intermediate_size=512, num_hidden_layers=2,
+                                   num_attention_heads=4, num_key_value_heads=4, vocab_size=64)
+    model = transformers.LlamaForCausalLM(cfg)
+    P.patch_mlp_with_block_circulant(model, num_layers_to_patch=1, block_size=64)
+    keys = sorted(model.state_dict().keys())
+    assert P.fuse_mlp_gate_up(model) == 1           # only the patched layer qualifies
+    assert sorted(model.state_dict().keys()) == keys
+    assert isinstance(model.model.layers[0].mlp._bc_gate_up, P.BCFusedGateUp)
