@@ -119,6 +119,38 @@ def time_spectra(layer, iters=20):
     return s.elapsed_time(e) / iters
 
 
+def time_glu(dev, steps, k=4096, m=11008, b=128, n=8192, io="bf16"):
+    """Config 2's gate/up pair of a BC LLaMA MLP: h = silu(gate(x)) * up(x) as ONE fused launch
+    (bcfft_forward_glu) vs the unfused sequence (two BC forwards + torch SiLU and product)."""
+    from bcfft import ops
+    torch.manual_seed(2)
+    cg = (torch.randn(m // b, k // b, b, device=dev) * 0.01).to(DT[io])
+    cu = (torch.randn(m // b, k // b, b, device=dev) * 0.01).to(DT[io])
+    x = torch.randn(n, k, device=dev).to(DT[io])
+    sgu, sg, su = ops.spectra(ops.glu_weights(cg, cu)), ops.spectra(cg), ops.spectra(cu)
+
+    def run(fn):
+        for _ in range(5):
+            fn()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(steps):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / steps
+
+    with torch.inference_mode():
+        fused = run(lambda: ops.forward_glu(x, sgu, b, m))
+        unfused = run(lambda: torch.nn.functional.silu(ops.forward(x, sg, None, b, m)) * ops.forward(x, su, None, b, m))
+    nbytes = n * k * SZ[io] + n * m * SZ[io] + 2 * (m // b) * (k // b) * (b // 2 + 1) * 8
+    return {"workload": f"gate/up {k}->{m} b={b} N={n} {io}-io + SwiGLU", "engine": "stationary-glu",
+            "ms": round(fused, 4), "unfused_ms": round(unfused, 4),
+            "GB_s": round(nbytes / (fused * 1e-3) / 1e9, 1),
+            "frac": round(nbytes / (fused * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
 def load_traffic(tag):
     """Per-launch HBM bytes from the newest profiles/pmc_traffic_*.json for this workload."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic_*.json")))
@@ -220,6 +252,7 @@ def main():
                              "GB_s": round(vbytes / (vkern * 1e-3) / 1e9, 1),
                              "frac": round(vbytes / (vkern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
             del vl, vx
+        variants.append(time_glu(dev, max(10, args.steps // 2)))
     wall, kern = time_layer(layer, x, args.steps, args.warmup, barrier)
     t = torch.tensor([wall, kern], device=dev, dtype=torch.float64)
     if world > 1:
