@@ -113,6 +113,32 @@ int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_feat
 int bcfft_forward_glu(const void* x, int x_dtype, int64_t n_tokens, int in_features, int gate_features,
                       int block_size, const void* spectra_gu, void* h, void* stream);
 
+/* Loss-aware circulant projection of a dense weight. Replaces the per-block
+ * Python loop of BlockCirculantLinear.from_linear (patch_llama_fft.py:207-219) over
+ * dense_block_to_circulant_column_loss_aware (:82-128) with one launch:
+ *   c[j,i,t] = alpha_ji * mean_r W[j*b + r, i*b + (r - t) mod b],
+ *   alpha_ji = <W_ji, C(c)> / max(b * sum_t c[t]^2, 1e-12)
+ * in the reference's arithmetic: every elementwise result rounded to w_dtype, reductions
+ * accumulated wider and rounded once (fp16 weights: bit-identical to the reference's CPU loop
+ * on its golden vectors).
+ *   w: (out_features, in_features) row-major, w_dtype; c: (out/b, in/b, b) fp32 (the module's
+ *   parameter dtype, :219). */
+int bcfft_project_circulant(const void* w, int w_dtype, int out_features, int in_features, int block_size,
+                            float* c, void* stream);
+
+/* Workspace bytes bcfft_grad_c needs for these sizes (0 when n_tokens == 0). */
+int64_t bcfft_grad_c_workspace_bytes(int64_t n_tokens, int in_features, int out_features, int block_size);
+
+/* Gradient of the BC forward with respect to c: what torch autograd computes
+ * through patch_llama_fft.py:246-271 for calibrate_bc.py:253-299,
+ *   dc[o,i,:] = irfft( sum_n rfft(dy[n,o]) * conj(rfft(x[n,i])) )   (circular cross-correlation)
+ * fp32 FFTs and accumulation, splits summed in fp64 in a fixed order (deterministic).
+ *   x: (n_tokens, in_features) x_dtype; dy: (n_tokens, out_features) dy_dtype; both 16-B aligned
+ *   workspace: bcfft_grad_c_workspace_bytes(...) bytes, 16-B aligned (may be NULL if 0)
+ *   dc: (out/b, in/b, b) of dc_dtype (the parameter's dtype), fully overwritten. */
+int bcfft_grad_c(const void* x, int x_dtype, const void* dy, int dy_dtype, int64_t n_tokens, int in_features,
+                 int out_features, int block_size, void* workspace, void* dc, int dc_dtype, void* stream);
+
 /* Single circulant matvec y = C(c) x, C[i,j] = c[(i-j) mod n], any n >= 1.
  * Replaces fft_utils.circulant_matvec_fft (fft_utils.py:3-34); c, x, y share `dtype`.
  * Direct O(n^2) evaluation accumulated in fp64 (this entry point serves validation-sized

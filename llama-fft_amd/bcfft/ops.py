@@ -121,6 +121,48 @@ def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, bl
     return y
 
 
+def _aligned(t: torch.Tensor) -> torch.Tensor:
+    t = t.contiguous()
+    return t.clone() if t.data_ptr() % 16 else t
+
+
+def project_circulant(weight: torch.Tensor, block_size: int) -> torch.Tensor:
+    """Loss-aware circulant projection of a dense device weight (out_f, in_f) -> c (nO, nI, b)
+    fp32 in one launch (bcfft_project_circulant): from_linear's per-block loop,
+    patch_llama_fft.py:207-219 over :82-128, with arithmetic in the weight's dtype."""
+    _lib.require_device(weight, "bcfft.project_circulant")
+    if weight.dim() != 2:
+        raise ValueError("weight must be (out_features, in_features)")
+    m, k = weight.shape
+    b = block_size
+    w = _aligned(weight.detach())
+    c = torch.empty((m // b, k // b, b), dtype=torch.float32, device=w.device)
+    lib = _lib.load()
+    _lib.check(lib.bcfft_project_circulant(w.data_ptr(), _lib.dtype_code(w.dtype), m, k, b, c.data_ptr(),
+                                           _lib.stream_handle(w.device)), "bcfft_project_circulant")
+    return c
+
+
+def grad_c(x2d: torch.Tensor, dy: torch.Tensor, block_size: int, c_dtype: torch.dtype = torch.float32) -> torch.Tensor:
+    """dL/dc of y = BC(x2d) for upstream gradient dy (N, out_f): (nO, nI, b) of c_dtype
+    (bcfft_grad_c; the autograd of patch_llama_fft.py:246-271 with respect to c)."""
+    _lib.require_device(x2d, "bcfft.grad_c")
+    n, k = x2d.shape
+    m = dy.shape[1]
+    b = block_size
+    x2d, dy = _aligned(x2d), _aligned(dy)
+    lib = _lib.load()
+    nbytes = lib.bcfft_grad_c_workspace_bytes(n, k, m, b)
+    if nbytes < 0:
+        raise ValueError(f"invalid grad_c geometry (N={n}, K={k}, M={m}, b={b})")
+    ws = torch.empty(max(nbytes // 4, 4), dtype=torch.float32, device=x2d.device)
+    dc = torch.empty((m // b, k // b, b), dtype=c_dtype, device=x2d.device)
+    _lib.check(lib.bcfft_grad_c(x2d.data_ptr(), _lib.dtype_code(x2d.dtype), dy.data_ptr(), _lib.dtype_code(dy.dtype),
+                                n, k, m, b, ws.data_ptr(), dc.data_ptr(), _lib.dtype_code(c_dtype),
+                                _lib.stream_handle(x2d.device)), "bcfft_grad_c")
+    return dc
+
+
 def circulant_matvec(c: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     """y = C(c) x for one circulant of any length (fft_utils.py:3-34)."""
     _lib.require_device(x, "bcfft.circulant_matvec")

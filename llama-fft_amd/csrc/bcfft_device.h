@@ -437,4 +437,14 @@ bool launch_forward_glu(int b, int n_in, int xdt, const void* x, int64_t n, int 
                         void* h, hipStream_t s);
 void launch_stat_image(int b, int n_out, int n_in, void* spec, hipStream_t s);
 
+// weight prep (bcfft_prep.hip): loss-aware circulant projection of a dense (n_out*b, n_in*b)
+// weight into c (n_out, n_in, b) fp32; false for an unsupported block size
+bool launch_project(int b, const void* w, int dt, int n_out, int n_in, float eps, float* c, hipStream_t s);
+
+// dc of the BC forward (bcfft_grad.hip): token split and workspace of the two-launch reduction
+struct GradPlan { int64_t tiles, splits, tokens_per_split, workspace_bytes; };
+GradPlan grad_plan(int b, int64_t n, int n_in, int n_out);
+void launch_grad_c(int b, const void* x, int x_dt, const void* dy, int dy_dt, int64_t n, int n_in, int n_out,
+                   void* ws, void* dc, int dc_dt, hipStream_t s);
+
 }  // namespace bcfft

@@ -719,6 +719,41 @@ int bcfft_set_stamps(void* buf) {
 }
 #endif
 
+int bcfft_project_circulant(const void* w, int w_dtype, int out_features, int in_features, int block_size,
+                            float* c, void* stream) {
+  if (!valid_block(block_size)) return BCFFT_ERR_BLOCK;
+  if (out_features <= 0 || in_features <= 0 || out_features % block_size || in_features % block_size)
+    return BCFFT_ERR_SHAPE;
+  if (!valid_dt(w_dtype)) return BCFFT_ERR_DTYPE;
+  if (!w || !c) return BCFFT_ERR_ARG;
+  bcfft::launch_project(block_size, w, w_dtype, out_features / block_size, in_features / block_size, 1e-12f, c,
+                        (hipStream_t)stream);
+  return record_launch();
+}
+
+int64_t bcfft_grad_c_workspace_bytes(int64_t n_tokens, int in_features, int out_features, int block_size) {
+  if (!valid_block(block_size) || n_tokens < 0 || in_features <= 0 || out_features <= 0 ||
+      in_features % block_size || out_features % block_size)
+    return -1;
+  return bcfft::grad_plan(block_size, n_tokens, in_features / block_size, out_features / block_size).workspace_bytes;
+}
+
+int bcfft_grad_c(const void* x, int x_dtype, const void* dy, int dy_dtype, int64_t n_tokens, int in_features,
+                 int out_features, int block_size, void* workspace, void* dc, int dc_dtype, void* stream) {
+  if (!valid_block(block_size)) return BCFFT_ERR_BLOCK;
+  if (n_tokens < 0 || in_features <= 0 || out_features <= 0 || in_features % block_size ||
+      out_features % block_size)
+    return BCFFT_ERR_SHAPE;
+  if (!valid_dt(x_dtype) || !valid_dt(dy_dtype) || !valid_dt(dc_dtype)) return BCFFT_ERR_DTYPE;
+  if (!dc || (n_tokens > 0 && (!x || !dy))) return BCFFT_ERR_ARG;
+  const int n_in = in_features / block_size, n_out = out_features / block_size;
+  if (bcfft::grad_plan(block_size, n_tokens, n_in, n_out).workspace_bytes > 0 && !workspace) return BCFFT_ERR_ARG;
+  if ((x && !aligned16(x)) || (dy && !aligned16(dy)) || (workspace && !aligned16(workspace))) return BCFFT_ERR_ALIGN;
+  bcfft::launch_grad_c(block_size, x, x_dtype, dy, dy_dtype, n_tokens, n_in, n_out, workspace, dc, dc_dtype,
+                       (hipStream_t)stream);
+  return record_launch();
+}
+
 int bcfft_circulant_matvec(const void* c, const void* x, int dtype, int n, void* y, void* stream) {
   if (!c || !x || !y) return BCFFT_ERR_ARG;
   if (n <= 0) return BCFFT_ERR_SHAPE;

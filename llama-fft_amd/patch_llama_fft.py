@@ -104,7 +104,7 @@ def circulant_from_first_col(c: torch.Tensor) -> torch.Tensor:
 # ----------------------------------------------------------------------------- autograd
 class _BCFunction(torch.autograd.Function):
     """Fused forward on the HIP engine; backward: dx through the fused kernel on adjoint
-    spectra, dc by per-bin cross-correlation (torch.fft on device), dbias by reduction."""
+    spectra, dc by the per-bin cross-correlation kernel (bcfft_grad_c), dbias by reduction."""
 
     @staticmethod
     def forward(ctx, x2d, c, bias, module):
@@ -124,12 +124,7 @@ class _BCFunction(torch.autograd.Function):
             spec_t = m._spectra(c, adjoint=True)
             dx = _ops.forward(dy, spec_t, None, m.block_size, m.in_features).to(x2d.dtype)
         if ctx.needs_input_grad[1]:
-            n = x2d.shape[0]
-            b = m.block_size
-            xf = torch.fft.rfft(x2d.to(torch.float32).reshape(n, m.in_blocks, b), dim=-1)
-            dyf = torch.fft.rfft(dy.to(torch.float32).reshape(n, m.out_blocks, b), dim=-1)
-            dcf = torch.einsum("nof,nif->oif", dyf, xf.conj())
-            dc = torch.fft.irfft(dcf, n=b, dim=-1).to(c.dtype)
+            dc = _ops.grad_c(x2d, dy, m.block_size, c.dtype)
         if bias is not None and ctx.needs_input_grad[2]:
             dbias = dy.sum(dim=0).to(bias.dtype)
         return dx, dc, dbias, None
@@ -170,8 +165,11 @@ class BlockCirculantLinear(nn.Module):
         with torch.no_grad():
             W = linear.weight.data
             B = block_size
-            blocks = W.view(layer.out_blocks, B, layer.in_blocks, B).permute(0, 2, 1, 3)       # :208-209
-            layer.c.data.copy_(_project_loss_aware_batched(blocks))                            # :214-219
+            if W.device.type == "cuda":                                                        # one launch
+                layer.c.data.copy_(_ops.project_circulant(W, B))                               # :207-219
+            else:                                                                              # host weights
+                blocks = W.view(layer.out_blocks, B, layer.in_blocks, B).permute(0, 2, 1, 3)   # :208-209
+                layer.c.data.copy_(_project_loss_aware_batched(blocks))                        # :214-219
             if layer.bias is not None and linear.bias is not None:
                 layer.bias.data.copy_(linear.bias.data)                                        # :221-222
         return layer

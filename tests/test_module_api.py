@@ -39,7 +39,7 @@ def test_default_block_size(plf):
 @pytest.mark.parametrize("name", names("from_linear_"))
 def test_from_linear_vs_reference_golden(plf, name):
     g = load(name)
-    dt = {"float32": torch.float32, "float16": torch.float16}[g["w__dt"]]
+    dt = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16}[g["w__dt"]]
     m, k = g["w"].shape
     lin = torch.nn.Linear(k, m, bias="lin_bias" in g).to(dt)
     with torch.no_grad():

@@ -65,6 +65,36 @@ def test_from_linear_golden(name):
     assert np.max(np.abs(c - g["c"])) < (1e-5 if d == O.F32 else 1e-3)
 
 
+@pytest.mark.parametrize("name", names("from_linear_"))
+def test_from_linear_16bit_bit_exact(name):
+    """16-bit weights: the oracle reproduces the reference's CPU loop bit for bit."""
+    g = load(name)
+    if g["w__dt"] == "float32":
+        pytest.skip("fp32 reductions differ in summation order (checked to 1e-5 above)")
+    c = O.from_linear_c(g["w"], int(g["block_size"]), DT[g["w__dt"]])
+    assert np.array_equal(c, g["c"])
+
+
+@pytest.mark.parametrize("name", names("bwd_"))
+def test_backward_golden(name):
+    """bc_grad_c / bc_grad_x against torch autograd through the reference forward
+    (tests/golden/make_golden_grad.py)."""
+    g = load(name)
+    b = int(g["block_size"])
+    x = g["x"].reshape(-1, g["x"].shape[-1])
+    dy = g["dy"].reshape(x.shape[0], -1)
+    dc = O.round_to(O.bc_grad_c(x, dy, b), DT[g["dc__dt"]])
+    dx = O.bc_grad_x(dy, g["c"], DT[g["x__dt"]])
+    if g["dc__dt"] == "float32":
+        assert rel_err(dc, g["dc"]) < 1e-6
+    else:
+        assert np.array_equal(dc, g["dc"])
+    tol = 1e-6 if g["x__dt"] == "float32" else 2e-3
+    assert rel_err(dx, g["dx"].reshape(dx.shape)) < tol
+    if "dbias" in g:
+        assert rel_err(O.round_to(dy.sum(0), DT[g["dbias__dt"]]), g["dbias"]) < 1e-6
+
+
 def test_project_t2_exact():
     """validate_implementation.py:47-78 — projection of a true circulant recovers c up to alpha."""
     g = load("project_t2_exact")
