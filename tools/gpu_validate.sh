@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_all.log 2>&1 &&
+timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1 &&
+timeout -k 10 300 python -u bench.py > gpurun_out/bench.log 2>&1 &&
+cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof --output-format csv -o run -- python3 $GRAFT_REPO_ROOT/tools/time_grad_prep.py > $GRAFT_REPO_ROOT/gpurun_out/prof_grad.log 2>&1
