@@ -19,6 +19,10 @@
 // x and dy read (nO/TO and nI/TI times from L2) plus the workspace.
 #include "bcfft_device.h"
 
+#ifndef BCFFT_GRAD_ABL
+#define BCFFT_GRAD_ABL 0   // analysis builds only: 1 skip MACs, 2 skip FFTs, 4 skip global loads
+#endif
+
 namespace bcfft {
 
 template <int B>
@@ -102,7 +106,7 @@ __global__ __launch_bounds__(256) void bc_grad_c_kernel(const void* __restrict__
       const int t = r / RPT, bl = r % RPT;
       const int64_t n = n0 + t;
       float e[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (n < ne) {
+      if (n < ne && !(BCFFT_GRAD_ABL & 4)) {
         if (bl < G::TI) {
           if (i0 + bl < n_in) load8(x, n * K + (int64_t)(i0 + bl) * B + 8 * v, x_dt, e);
         } else if (o0 + bl - G::TI < n_out) {
@@ -114,7 +118,7 @@ __global__ __launch_bounds__(256) void bc_grad_c_kernel(const void* __restrict__
       *reinterpret_cast<float4*>(d + 4) = make_float4(e[4], e[5], e[6], e[7]);
     }
     __syncthreads();
-    for (int r = g; r < G::ROWS; r += G::NG) {      // whole waves take the same trip count
+    for (int r = g; r < G::ROWS && !(BCFFT_GRAD_ABL & 2); r += G::NG) {   // whole waves: same trip count
       float* row = rows + r * SROW;
       F::template forward<BCFFT_F32>(row, gl, tw);
       // untangle in place: the lane that reads Z[k] and Z[H-k] writes X'[k] and X'[H-k]
@@ -138,7 +142,7 @@ __global__ __launch_bounds__(256) void bc_grad_c_kernel(const void* __restrict__
     }
     __syncthreads();
 #pragma unroll 1
-    for (int t = 0; t < TT; ++t) {
+    for (int t = 0; t < TT && !(BCFFT_GRAD_ABL & 1); ++t) {
       const float* rt = rows + t * RPT * SROW + 2 * f;
       float xr[G::SI], xa[G::SI], xb[G::SI];
 #pragma unroll
@@ -172,47 +176,73 @@ __global__ __launch_bounds__(256) void bc_grad_c_kernel(const void* __restrict__
 template <int B>
 __global__ __launch_bounds__(256) void bc_grad_c_finish(const float2* __restrict__ ws, int n_splits,
                                                         int n_out, int n_in, int dc_dt, void* __restrict__ dc) {
-  constexpr int H = B / 2;
-  __shared__ double ar[H], ai[H], cs[B], sn[B];
+  // per block (o, i): 256 threads = H bins x SG split groups. Thread (k, sg) sums splits
+  // s = sg, sg + SG, ... (coalesced over k, 8 loads in flight); the SG partials are then added
+  // in a fixed order (deterministic).
+  constexpr int H = B / 2, SG = 256 / H;
+  __shared__ double pr[SG][H], pi[SG][H];
+  __shared__ double ar[H], ai[H];
   const int64_t blk = blockIdx.x;
-  const int tid = threadIdx.x;
-  for (int m = tid; m < B; m += blockDim.x) {
-    double s, c;
-    sincospi(2.0 * (double)m / (double)B, &s, &c);
-    cs[m] = c;
-    sn[m] = s;
-  }
+  const int tid = threadIdx.x, k = tid % H, sg = tid / H;
   const int64_t stride = (int64_t)n_out * n_in * H;
-  for (int k = tid; k < H; k += blockDim.x) {
-    double re = 0.0, im = 0.0;
-    for (int s = 0; s < n_splits; ++s) {
-      const float2 v = ws[s * stride + blk * H + k];
-      re += v.x;
-      im += v.y;
+  const float2* src = ws + blk * H + k;
+  double re = 0.0, im = 0.0;
+  int s = sg;
+  for (; s + 7 * SG < n_splits; s += 8 * SG) {
+    float2 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(s + u * SG) * stride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      re += v[u].x;
+      im += v[u].y;
     }
-    ar[k] = re;
-    ai[k] = im;
+  }
+  for (; s < n_splits; s += SG) {
+    const float2 v = src[(int64_t)s * stride];
+    re += v.x;
+    im += v.y;
+  }
+  pr[sg][k] = re;
+  pi[sg][k] = im;
+  __syncthreads();
+  if (tid < H) {
+    double a = 0.0, b = 0.0;
+#pragma unroll
+    for (int g = 0; g < SG; ++g) {
+      a += pr[g][tid];
+      b += pi[g][tid];
+    }
+    ar[tid] = a;
+    ai[tid] = b;
   }
   __syncthreads();
-  for (int t = tid; t < B; t += blockDim.x) {
-    double y = ar[0] + ((t & 1) ? -ai[0] : ai[0]);          // DC and Nyquist (packed bin 0)
-    for (int k = 1; k < H; ++k) {
-      const int m = (k * t) & (B - 1);
-      y += 2.0 * (ar[k] * cs[m] - ai[k] * sn[m]);
+  // inverse real DFT of the packed bins, fp64: y[t] = A0 + (-1)^t A_H + 2 sum_k Re(A_k e^{2 pi i k t / B});
+  // the per-t twiddle e^{2 pi i t / B} advances by a fp64 complex recurrence (error ~H ulp of fp64)
+  for (int t = tid; t < B; t += 256) {
+    double st, ct;
+    sincospi(2.0 * (double)t / (double)B, &st, &ct);
+    double wr = ct, wi = st, acc = 0.0;
+    for (int kk = 1; kk < H; ++kk) {
+      acc += ar[kk] * wr - ai[kk] * wi;
+      const double nr = wr * ct - wi * st;
+      wi = wr * st + wi * ct;
+      wr = nr;
     }
+    const double y = ar[0] + ((t & 1) ? -ai[0] : ai[0]) + 2.0 * acc;
     const float v = (float)(y / (4.0 * B));
     if (dc_dt == BCFFT_F32) ((float*)dc)[blk * B + t] = v;
     else ((uint16_t*)dc)[blk * B + t] = (uint16_t)(dc_dt == BCFFT_BF16 ? f32_to_bf16(v) : f32_to_f16(v));
   }
 }
 
-// token split: enough workgroups to fill the chip twice over, at least one sub-batch each
+// token split: two workgroups per CU (their LDS / VGPR limit), at least one sub-batch each
 template <int B>
 GradPlan grad_plan_b(int64_t n, int n_in, int n_out) {
   using G = GeoG<B>;
   GradPlan p;
   p.tiles = (int64_t)((n_out + G::TO - 1) / G::TO) * ((n_in + G::TI - 1) / G::TI);
-  int64_t s = (1024 + p.tiles - 1) / p.tiles;
+  int64_t s = (512 + p.tiles - 1) / p.tiles;
   const int64_t sub = (n + G::TT - 1) / G::TT;
   if (s > sub) s = sub;
   if (s < 1) s = 1;
@@ -239,7 +269,7 @@ void launch_grad_c_b(const void* x, int x_dt, const void* dy, int dy_dt, int64_t
   if (p.splits > 0)
     hipLaunchKernelGGL(bc_grad_c_kernel<B>, dim3((unsigned)p.tiles, (unsigned)p.splits), dim3(GeoG<B>::NT), 0, s,
                        x, x_dt, dy, dy_dt, n, n_in, n_out, p.tokens_per_split, (float2*)ws);
-  hipLaunchKernelGGL(bc_grad_c_finish<B>, dim3((unsigned)((int64_t)n_out * n_in)), dim3(B < 64 ? 64 : B), 0, s,
+  hipLaunchKernelGGL(bc_grad_c_finish<B>, dim3((unsigned)((int64_t)n_out * n_in)), dim3(256), 0, s,
                      (const float2*)ws, (int)p.splits, n_out, n_in, dc_dt, dc);
 }
 
