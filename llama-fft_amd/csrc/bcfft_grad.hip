@@ -67,7 +67,8 @@ template <int B>
 __global__ __launch_bounds__(256) void bc_grad_c_kernel(const void* __restrict__ x, int x_dt,
                                                         const void* __restrict__ dy, int dy_dt,
                                                         int64_t n_tokens, int n_in, int n_out,
-                                                        int64_t tokens_per_split, float2* __restrict__ ws) {
+                                                        int64_t tokens_per_split, int64_t n_splits,
+                                                        float2* __restrict__ ws) {
   using G = GeoG<B>;
   using F = Fft<B>;
   constexpr int H = G::H, L = G::L, SROW = G::SROW, TT = G::TT, RPT = G::RPT;
@@ -77,8 +78,16 @@ __global__ __launch_bounds__(256) void bc_grad_c_kernel(const void* __restrict__
 
   const int tid = threadIdx.x;
   const int n_ti = (n_in + G::TI - 1) / G::TI;
-  const int o0 = (int)(blockIdx.x / n_ti) * G::TO, i0 = (int)(blockIdx.x % n_ti) * G::TI;
-  const int64_t nb = (int64_t)blockIdx.y * tokens_per_split;
+  const int n_tiles = ((n_out + G::TO - 1) / G::TO) * n_ti;
+  // XCD-aware 1-D grid: blocks b and b + 8 share an XCD (and its L2), so the n_tiles
+  // workgroups of one token split are blocks 8 q + xcd of consecutive q: they read the same
+  // x / dy rows close in time through one L2 (each row is read by nO/TO resp. nI/TI tiles)
+  const int64_t bq = blockIdx.x >> 3;
+  const int tile = (int)(bq % n_tiles);
+  const int64_t split = (bq / n_tiles) * 8 + (blockIdx.x & 7);
+  if (split >= n_splits) return;
+  const int o0 = (tile / n_ti) * G::TO, i0 = (tile % n_ti) * G::TI;
+  const int64_t nb = split * tokens_per_split;
   const int64_t ne = nb + tokens_per_split < n_tokens ? nb + tokens_per_split : n_tokens;
   const int64_t K = (int64_t)n_in * B, M = (int64_t)n_out * B;
 
@@ -163,7 +172,7 @@ __global__ __launch_bounds__(256) void bc_grad_c_kernel(const void* __restrict__
       }
     }
   }
-  const int64_t split_off = (int64_t)blockIdx.y * n_out * n_in;
+  const int64_t split_off = split * n_out * n_in;
 #pragma unroll
   for (int a = 0; a < G::SO; ++a)
 #pragma unroll
@@ -267,8 +276,8 @@ void launch_grad_c_b(const void* x, int x_dt, const void* dy, int dy_dt, int64_t
                      void* ws, void* dc, int dc_dt, hipStream_t s) {
   const GradPlan p = grad_plan_b<B>(n, n_in, n_out);
   if (p.splits > 0)
-    hipLaunchKernelGGL(bc_grad_c_kernel<B>, dim3((unsigned)p.tiles, (unsigned)p.splits), dim3(GeoG<B>::NT), 0, s,
-                       x, x_dt, dy, dy_dt, n, n_in, n_out, p.tokens_per_split, (float2*)ws);
+    hipLaunchKernelGGL(bc_grad_c_kernel<B>, dim3((unsigned)(p.tiles * ((p.splits + 7) / 8) * 8)), dim3(GeoG<B>::NT),
+                       0, s, x, x_dt, dy, dy_dt, n, n_in, n_out, p.tokens_per_split, p.splits, (float2*)ws);
   hipLaunchKernelGGL(bc_grad_c_finish<B>, dim3((unsigned)((int64_t)n_out * n_in)), dim3(256), 0, s,
                      (const float2*)ws, (int)p.splits, n_out, n_in, dc_dt, dc);
 }
