@@ -419,6 +419,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
   // 4 token rows are one contiguous span of x: a lane's source offset is its row byte with the
   // row's unit swizzle (swz_x) XORed in; the buffer range check zero-fills rows past n_tokens
   // (those tokens are never stored).
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
   auto dma_tile = [&](int64_t m, char* region) {
     if (wave >= NWF) return;
     const int64_t tok0 = m * TT;
@@ -438,9 +439,12 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
 #pragma unroll
     for (int c = 0; c < DP; ++c)
       vb[c] = wave * NDMA * 1024 + ((dlane * 16) ^ (swz_x<L, ES>(c * RPK + (dlane * 16) / RB) << 4));
+    // LDS byte address of the slot from the array's base: plain scalar adds, no generic-to-LDS
+    // conversion (and its null check) per piece
+    const uint32_t dst0 = lds_base + (uint32_t)(region - lds) + wave * SLOT;
 #pragma unroll
     for (int q = 0; q < NDMA; ++q) {
-      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(region + wave * SLOT + q * 1024));
+      const uint32_t dst = dst0 + q * 1024;
       uint32_t keep;
       asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
                    : "=&s"(keep) : "v"(vb[q % DP]), "s"(xrs), "s"(dst), "s"(q * 1024) : "memory");
