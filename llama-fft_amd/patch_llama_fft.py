@@ -396,6 +396,88 @@ def fuse_mlp_gate_up(model) -> int:
     return n
 
 
+class BCFusedProjections:
+    """Several BlockCirculantLinear projections of the SAME input (LLaMA's q/k/v) as ONE launch
+    over their concatenated weights: y = x [C_q; C_k; C_v]^T, split into views.
+    One launch runs every output group of the three at once, so at small token counts (decode,
+    short prompts) it takes about the time of one projection instead of three.
+
+    The projections keep their modules, parameters and state_dict; fuse_attention_qkv points
+    each module's forward here. The first call for an input computes all outputs; the others
+    return their views of it for the same input (same tensor, same version). Autograd or mixed
+    bias / dtype / block size use the modules' own forward."""
+
+    def __init__(self, mods):
+        self.mods = list(mods)
+        m0 = self.mods[0]
+        if any((m.in_features, m.block_size, m.c.dtype) != (m0.in_features, m0.block_size, m0.c.dtype)
+               for m in self.mods):
+            raise ValueError("fused projections need one in_features, block_size and weight dtype")
+        self.splits = [m.out_features for m in self.mods]
+        self._spec = self._key = None
+        self._x = self._ver = self._outs = None
+        self._left = set()
+
+    def _fused_ok(self, x: torch.Tensor) -> bool:
+        grad = torch.is_grad_enabled() and (x.requires_grad or any(
+            m.c.requires_grad or (m.bias is not None and m.bias.requires_grad) for m in self.mods))
+        biases = [m.bias is None for m in self.mods]
+        return x.is_cuda and not grad and (all(biases) or not any(biases))
+
+    def _weights(self):
+        key = tuple((m.c.data_ptr(), m.c._version) for m in self.mods) + (self.mods[0].c.device,)
+        if key != self._key:
+            self._spec = _ops.spectra(torch.cat([m.c.detach() for m in self.mods], dim=0))
+            self._bias = (None if self.mods[0].bias is None
+                          else torch.cat([m.bias.detach() for m in self.mods]))
+            self._key = key
+        return self._spec, self._bias
+
+    def output(self, idx: int, x: torch.Tensor) -> torch.Tensor:
+        m = self.mods[idx]
+        if not self._fused_ok(x):
+            return BlockCirculantLinear.forward(m, x)
+        if not (self._x is x and self._ver == x._version and idx in self._left):
+            spec, bias = self._weights()
+            shape = x.shape
+            if x.dim() not in (2, 3):
+                raise ValueError("Unsupported input dim")                              # :239
+            x2d = x.reshape(-1, shape[-1])
+            y = _ops.forward(x2d, spec, bias, m.block_size, sum(self.splits))
+            outs, o = [], 0
+            for n in self.splits:
+                outs.append(y[:, o:o + n].view(*shape[:-1], n))
+                o += n
+            self._x, self._ver, self._outs, self._left = x, x._version, outs, set(range(len(self.mods)))
+        out = self._outs[idx]
+        self._left.discard(idx)
+        if not self._left:                              # every view handed out: drop the input
+            self._x = self._outs = None
+        return out
+
+
+def fuse_attention_qkv(model) -> int:
+    """Route q_proj / k_proj / v_proj of each decoder layer whose three projections are
+    BlockCirculantLinear (patch_linear_with_block_circulant) through one BCFusedProjections
+    launch. Parameters and state_dict are unchanged. Returns the number of layers rewired."""
+    import types
+    n = 0
+    for layer in model.model.layers:
+        attn = getattr(layer, "self_attn", None)
+        mods = [getattr(attn, nm, None) for nm in ("q_proj", "k_proj", "v_proj")] if attn is not None else []
+        if len(mods) != 3 or not all(isinstance(m, BlockCirculantLinear) for m in mods):
+            continue
+        try:
+            fused = BCFusedProjections(mods)
+        except ValueError:
+            continue
+        for i, m in enumerate(mods):
+            m.forward = types.MethodType(lambda self, x, _f=fused, _i=i: _f.output(_i, x), m)
+        object.__setattr__(attn, "_bc_qkv", fused)
+        n += 1
+    return n
+
+
 def main():
     """patch_llama_fft.py:396-419 — load LLaMA from MODEL_PATH, patch, run a shape check."""
     from transformers import AutoModelForCausalLM

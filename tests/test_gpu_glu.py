@@ -123,3 +123,31 @@ def test_fused_mlp_module_matches_unfused(dev):
         assert P.fuse_mlp_gate_up(model) == 1
         out = model(input_ids=ids).logits.float()
     assert ((out - ref).norm() / ref.norm()).item() < 1e-3
+
+
+def test_fused_qkv_matches_unfused(dev):
+    """fuse_attention_qkv: q/k/v of a GQA LLaMA layer (k/v narrower than q) in one launch over the
+    concatenated weights, against the three separate launches (bit-identical per output block),
+    then a whole one-layer LLaMA's logits."""
+    transformers = pytest.importorskip("transformers")
+    import patch_llama_fft as P
+    torch.manual_seed(1)
+    cfg = transformers.LlamaConfig(hidden_size=2048, intermediate_size=5632, num_hidden_layers=1,
+                                   num_attention_heads=16, num_key_value_heads=4, vocab_size=256,
+                                   max_position_embeddings=64)
+    model = transformers.LlamaForCausalLM(cfg).eval()
+    P.patch_linear_with_block_circulant(model, num_layers_to_patch=1, block_size=128)
+    model = model.to(dev)
+    attn = model.model.layers[0].self_attn
+    x = torch.randn(3, 17, 2048, device=dev)
+    ids = torch.randint(0, 256, (2, 16), device=dev)
+    with torch.no_grad():
+        sep = [attn.q_proj(x), attn.k_proj(x), attn.v_proj(x)]
+        ref = model(input_ids=ids).logits.float()
+        assert P.fuse_attention_qkv(model) == 1
+        fused = [attn.q_proj(x), attn.k_proj(x), attn.v_proj(x)]
+        out = model(input_ids=ids).logits.float()
+    for a, b in zip(sep, fused):
+        assert a.shape == b.shape and torch.equal(a, b)
+    assert ((out - ref).norm() / ref.norm()).item() < 1e-6
+

@@ -147,3 +147,20 @@ def test_fuse_mlp_gate_up_rewires_without_new_parameters():
     assert P.fuse_mlp_gate_up(model) == 1           # only the patched layer qualifies
     assert sorted(model.state_dict().keys()) == keys
     assert isinstance(model.model.layers[0].mlp._bc_gate_up, P.BCFusedGateUp)
+
+
+def test_fuse_attention_qkv_rewires_without_new_parameters():
+    transformers = pytest.importorskip("transformers")
+    import patch_llama_fft as P
+    cfg = transformers.LlamaConfig(hidden_size=256, intermediate_size=512, num_hidden_layers=2,
+                                   num_attention_heads=4, num_key_value_heads=2, vocab_size=64)
+    model = transformers.LlamaForCausalLM(cfg)
+    P.patch_linear_with_block_circulant(model, num_layers_to_patch=1, block_size=64)
+    keys = sorted(model.state_dict().keys())
+    assert P.fuse_attention_qkv(model) == 1         # only the patched layer qualifies
+    assert sorted(model.state_dict().keys()) == keys
+    fused = model.model.layers[0].self_attn._bc_qkv
+    assert fused.splits == [256, 128, 128]          # GQA: k/v have num_key_value_heads * head_dim
+    with pytest.raises(RuntimeError, match="ROCm device"):   # no CPU path behind the fused route
+        model.model.layers[0].self_attn.q_proj(torch.zeros(2, 256))
+
