@@ -130,6 +130,15 @@ class _BCFunction(torch.autograd.Function):
         return dx, dc, dbias, None
 
 
+def _version_of(x: torch.Tensor):
+    """x's in-place version counter; None for inference tensors (created under
+    torch.inference_mode, as the reference's harnesses and model.generate run), which have none.
+    Caches keyed on it then match by storage identity alone: fused q/k/v outputs are dropped as
+    soon as every projection has taken its view, and the spectra of a c created in inference
+    mode are not refreshed by in-place edits of that c (edit it outside inference mode)."""
+    return None if x.is_inference() else x._version
+
+
 # ----------------------------------------------------------------------------- the module
 class BlockCirculantLinear(nn.Module):
     """Block-circulant linear layer (patch_llama_fft.py:142-275), FFT-multiplied on MI355X.
@@ -176,7 +185,7 @@ class BlockCirculantLinear(nn.Module):
 
     # -- spectra cache (device, storage, version, dtype): recomputed after any update of c
     def _spectra(self, c: torch.Tensor, adjoint: bool = False) -> torch.Tensor:
-        key = (adjoint, c.device, c.data_ptr(), c._version, c.dtype, tuple(c.shape))
+        key = (adjoint, c.device, c.data_ptr(), _version_of(c), c.dtype, tuple(c.shape))
         spec = self._spec_cache.get(key)
         if spec is None:
             self._spec_cache = {k: v for k, v in self._spec_cache.items() if k[0] != adjoint}
@@ -352,7 +361,7 @@ class BCFusedGateUp(nn.Module):
 
     def _spectra(self) -> torch.Tensor:
         g, u = self._gate.c, self._up.c
-        key = (g.device, g.data_ptr(), g._version, u.data_ptr(), u._version, g.dtype)
+        key = (g.device, g.data_ptr(), _version_of(g), u.data_ptr(), _version_of(u), g.dtype)
         if key != self._key:
             self._spec = _ops.spectra(_ops.glu_weights(g, u))
             self._key = key
@@ -425,7 +434,7 @@ class BCFusedProjections:
         return x.is_cuda and not grad and (all(biases) or not any(biases))
 
     def _weights(self):
-        key = tuple((m.c.data_ptr(), m.c._version) for m in self.mods) + (self.mods[0].c.device,)
+        key = tuple((m.c.data_ptr(), _version_of(m.c)) for m in self.mods) + (self.mods[0].c.device,)
         if key != self._key:
             self._spec = _ops.spectra(torch.cat([m.c.detach() for m in self.mods], dim=0))
             self._bias = (None if self.mods[0].bias is None
@@ -437,7 +446,8 @@ class BCFusedProjections:
         m = self.mods[idx]
         if not self._fused_ok(x):
             return BlockCirculantLinear.forward(m, x)
-        if not (self._x is x and self._ver == x._version and idx in self._left):
+        ver = _version_of(x)
+        if not (self._x is x and self._ver == ver and idx in self._left):
             spec, bias = self._weights()
             shape = x.shape
             if x.dim() not in (2, 3):
@@ -448,7 +458,7 @@ class BCFusedProjections:
             for n in self.splits:
                 outs.append(y[:, o:o + n].view(*shape[:-1], n))
                 o += n
-            self._x, self._ver, self._outs, self._left = x, x._version, outs, set(range(len(self.mods)))
+            self._x, self._ver, self._outs, self._left = x, ver, outs, set(range(len(self.mods)))
         out = self._outs[idx]
         self._left.discard(idx)
         if not self._left:                              # every view handed out: drop the input
