@@ -389,6 +389,9 @@ struct SpecLayout {
   int64_t packed_f2, tw_off_f2, img_off_u32, img_u32, stat_off_u32, stat_u32, total_bytes;
   int n_chunk, n_out_pad, stat_groups, stat_pieces;
 };
+#ifndef BCFFT_MFMA_MAXB
+#define BCFFT_MFMA_MAXB 128          // largest block size with a split-bf16 MFMA image
+#endif
 __host__ __device__ inline int mfma_out_per_wg(int b) { return 4096 / b; }   // 16 * NTL
 // stationary-weight kernel geometries: fp16 B fragments of 32 output blocks x all inputs fit
 // 128 VGPRs per lane of 8 waves (K <= 4096), and the A image swizzle needs >= 8 block quads
@@ -403,7 +406,7 @@ __host__ __device__ inline SpecLayout spec_layout(int n_out, int n_in, int b) {
   s.tw_off_f2 = s.packed_f2;
   const int64_t head_f2 = s.packed_f2 + b;
   s.img_off_u32 = head_f2 * 2;
-  if (b <= 128) {
+  if (b <= BCFFT_MFMA_MAXB) {
     const int opw = mfma_out_per_wg(b);
     s.n_chunk = (n_in + 7) / 8;
     s.n_out_pad = (n_out + opw - 1) / opw * opw;

@@ -265,7 +265,7 @@ struct GeoM {
   static_assert(BPW * NTL * 4 == 128, "accumulator budget");
   static_assert(HROWS % NW == 0 && EPI_ROWS % NGROUPS == 0, "row tiling");
   static_assert(H >= 16, "bin swizzle needs H >= 16");
-  static_assert(LDS_FLOATS * 4 <= 80 * 1024, "LDS budget: two workgroups per CU");
+  static_assert(LDS_FLOATS * 4 <= (B <= 128 ? 80 : 160) * 1024, "LDS budget: two workgroups per CU (b <= 128)");
 };
 
 template <int B, int XT, bool YF32>
@@ -558,7 +558,7 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 template <int B, int XT, bool YF32>
 void launch_forward(int algo, const void* x, int64_t n, int n_in, int n_out, const void* spec,
                     const void* bias, int bias_dt, void* y, hipStream_t s) {
-  if constexpr (B <= 128) {
+  if constexpr (B <= BCFFT_MFMA_MAXB) {
     if (algo == BCFFT_ALGO_MFMA) {
       using G = bcfft::GeoM<B>;
       dim3 grid((unsigned)((n + G::TT - 1) / G::TT), (unsigned)((n_out + G::OUT_PER_WG - 1) / G::OUT_PER_WG));
@@ -591,7 +591,7 @@ void launch_spectra(const void* c, int c_dt, int n_out, int n_in, int tc, float2
   const unsigned threads = (B / 2) < 64 ? 64u : (unsigned)(B / 2);
   hipLaunchKernelGGL(bcfft::bc_spectra_kernel<B>, dim3(nblk), dim3(threads), 0, s, c, c_dt,
                      n_out, n_in, tc, out);
-  if constexpr (B <= 128) {
+  if constexpr (B <= BCFFT_MFMA_MAXB) {
     const bcfft::SpecLayout sl = bcfft::spec_layout(n_out, n_in, B);
     const int64_t total = sl.img_u32 / 2;
     const unsigned blocks = (unsigned)((total + 255) / 256 < 65535 ? (total + 255) / 256 : 65535);
