@@ -100,6 +100,24 @@ int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_feat
                        int out_features, int block_size, const void* spectra, const void* bias,
                        int bias_dtype, void* y, int y_dtype, int algo, void* stream);
 
+/* Optional workspace of bcfft_forward_ws, in bytes (0: the forward never uses one; < 0:
+ * invalid geometry). Non-zero only where the split-bf16 MFMA kernel (algo, AUTO resolved) runs a
+ * grid shorter than the device's CU count (n_tokens < 8 x CUs) over >= 32 input blocks, e.g.
+ * LLaMA's 11008 -> 4096 down projection at prefill and decode sizes: it then splits the input
+ * blocks over kz >= 2 workgroup slices (as many as fill two workgroups per CU, >= 2 chunks of 8
+ * input blocks each) that write fp32 partial outputs to the workspace (kz x n_tokens x
+ * out_features floats), and a finishing pass adds them in a fixed order and applies the
+ * epilogue: bit-reproducible, and identical per output block for q/k/v-style concatenations. */
+int64_t bcfft_forward_workspace_bytes(int64_t n_tokens, int in_features, int out_features, int block_size,
+                                      int algo);
+
+/* bcfft_forward_algo with a caller-owned device workspace (16-B aligned), used when
+ * workspace_bytes >= bcfft_forward_workspace_bytes(...); NULL / too small runs unsplit. */
+int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_features,
+                     int out_features, int block_size, const void* spectra, const void* bias,
+                     int bias_dtype, void* y, int y_dtype, int algo, void* workspace,
+                     int64_t workspace_bytes, void* stream);
+
 /* Fused gate/up projections + SwiGLU of a LLaMA MLP (the reference MLP
  * computes down(act(gate(x)) * up(x)) with gate/up BC-patched by patch_llama_fft.py:343-394;
  * act = SiLU): h = silu(BC_gate(x)) * BC_up(x) in ONE launch, without writing gate(x) and up(x)

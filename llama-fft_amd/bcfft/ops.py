@@ -114,9 +114,13 @@ def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, bl
         bias_ptr, bias_code = bias.data_ptr(), _lib.dtype_code(bias.dtype)
     lib = _lib.load()
     code = _lib.ALGOS[(algo or default_algo()).lower()]
-    _lib.check(lib.bcfft_forward_algo(x2d.data_ptr(), _lib.dtype_code(x2d.dtype), n, k, out_features,
-                                      block_size, spec.data_ptr(), bias_ptr, bias_code, y.data_ptr(),
-                                      _lib.dtype_code(out_dtype), code, _lib.stream_handle(x2d.device)),
+    # split-K workspace (short grids of the MFMA kernel); caller-owned, from torch's allocator
+    ws_bytes = lib.bcfft_forward_workspace_bytes(n, k, out_features, block_size, code)
+    ws = torch.empty(max(ws_bytes, 0), dtype=torch.uint8, device=x2d.device) if ws_bytes > 0 else None
+    _lib.check(lib.bcfft_forward_ws(x2d.data_ptr(), _lib.dtype_code(x2d.dtype), n, k, out_features,
+                                    block_size, spec.data_ptr(), bias_ptr, bias_code, y.data_ptr(),
+                                    _lib.dtype_code(out_dtype), code, 0 if ws is None else ws.data_ptr(),
+                                    max(ws_bytes, 0), _lib.stream_handle(x2d.device)),
                "bcfft_forward")
     return y
 

@@ -214,6 +214,37 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// four consecutive fp32 outputs y32[off .. off+3] of a BC forward -> y, with the reference's
+// roundings (patch_llama_fft.py:266-271): .to(x dtype), + bias in fp32, rounded to the y dtype
+// (= promote(x dtype, bias dtype): the x dtype, or fp32 when YF32). bias is 16-B aligned.
+template <int XT, bool YF32>
+__device__ __forceinline__ void store4(float4 val, void* yv, int64_t off, const void* bias, int64_t bcol,
+                                       int bias_dt) {
+  float vv[4] = {round_to(val.x, XT), round_to(val.y, XT), round_to(val.z, XT), round_to(val.w, XT)};
+  if (bias_dt != BCFFT_NONE) {
+    float bb[4];
+    if (bias_dt == BCFFT_F32) {
+      const float4 b4 = *reinterpret_cast<const float4*>((const float*)bias + bcol);
+      bb[0] = b4.x; bb[1] = b4.y; bb[2] = b4.z; bb[3] = b4.w;
+    } else {
+      const uint2 b2 = *reinterpret_cast<const uint2*>((const uint16_t*)bias + bcol);
+      const uint32_t w[4] = {b2.x & 0xffffu, b2.x >> 16, b2.y & 0xffffu, b2.y >> 16};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bb[e] = bias_dt == BCFFT_BF16 ? bf16_to_f32(w[e]) : f16_to_f32(w[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) vv[e] += bb[e];
+  }
+  if constexpr (YF32 || XT == BCFFT_F32) {
+    *reinterpret_cast<float4*>((float*)yv + off) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+  } else {
+    uint32_t h[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) h[e] = XT == BCFFT_BF16 ? f32_to_bf16(vv[e]) : f32_to_f16(vv[e]);
+    *reinterpret_cast<uint2*>((uint16_t*)yv + off) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+  }
+}
+
 // ------------------------------------------------------------------ FFT building blocks
 // One transform per L-lane group, on an LDS row of SROW floats.
 template <int B>
@@ -320,31 +351,17 @@ struct Fft {
 #pragma unroll
     for (int pc = 0; pc < B / (4 * L); ++pc) {
       const int p4 = (gl + L * pc) * 4;
-      const float4 val = *reinterpret_cast<const float4*>(row + p4);
-      float vv[4] = {round_to(val.x, XT), round_to(val.y, XT), round_to(val.z, XT),   // .to(x.dtype) :266
-                     round_to(val.w, XT)};
-      if (bias_dt != BCFFT_NONE) {                                                   // + bias :270-271
-        float bb[4];
-        if (bias_dt == BCFFT_F32) {
-          const float4 b4 = *reinterpret_cast<const float4*>((const float*)bias + bcol + p4);
-          bb[0] = b4.x; bb[1] = b4.y; bb[2] = b4.z; bb[3] = b4.w;
-        } else {
-          const uint2 b2 = *reinterpret_cast<const uint2*>((const uint16_t*)bias + bcol + p4);
-          const uint32_t w[4] = {b2.x & 0xffffu, b2.x >> 16, b2.y & 0xffffu, b2.y >> 16};
+      store4<XT, YF32>(*reinterpret_cast<const float4*>(row + p4), yv, off + p4, bias, bcol + p4, bias_dt);
+    }
+  }
+
+  // split-K partial: one transform's b fp32 outputs to the slice's workspace row (plain 16-B
+  // stores; the finishing pass adds the slices in a fixed order)
+  static __device__ __forceinline__ void store_partial(const float* row, int gl, float* dst) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) bb[e] = bias_dt == BCFFT_BF16 ? bf16_to_f32(w[e]) : f16_to_f32(w[e]);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) vv[e] += bb[e];
-      }
-      if constexpr (YF32 || XT == BCFFT_F32) {
-        *reinterpret_cast<float4*>((float*)yv + off + p4) = make_float4(vv[0], vv[1], vv[2], vv[3]);
-      } else {
-        uint32_t h[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) h[e] = XT == BCFFT_BF16 ? f32_to_bf16(vv[e]) : f32_to_f16(vv[e]);
-        *reinterpret_cast<uint2*>((uint16_t*)yv + off + p4) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
-      }
+    for (int pc = 0; pc < B / (4 * L); ++pc) {
+      const int p4 = (gl + L * pc) * 4;
+      *reinterpret_cast<float4*>(dst + p4) = *reinterpret_cast<const float4*>(row + p4);
     }
   }
 };
@@ -389,6 +406,7 @@ struct SpecLayout {
   int64_t packed_f2, tw_off_f2, img_off_u32, img_u32, stat_off_u32, stat_u32, total_bytes;
   int n_chunk, n_out_pad, stat_groups, stat_pieces;
 };
+int device_cu_count();         // CUs of the current device (bcfft_stat.hip)
 #ifndef BCFFT_MFMA_MAXB
 #define BCFFT_MFMA_MAXB 128          // largest block size with a split-bf16 MFMA image
 #endif

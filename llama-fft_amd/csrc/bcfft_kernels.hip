@@ -272,7 +272,7 @@ template <int B, int XT, bool YF32>
 __global__ __launch_bounds__(256, 2) void bc_forward_mfma_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_in, int n_out,
     const float2* __restrict__ spec, const void* __restrict__ bias, int bias_dt,
-    void* __restrict__ yv) {
+    void* __restrict__ yv, float* __restrict__ yacc) {
   using G = GeoM<B>;
   using F = Fft<B>;
   constexpr int H = G::H, L = G::L, TT = G::TT, KB = G::KB, KH = G::KH, SROW = G::SROW, XS = G::XS;
@@ -363,14 +363,19 @@ __global__ __launch_bounds__(256, 2) void bc_forward_mfma_kernel(
     dst[1] = *reinterpret_cast<const uint4*>(p + prec_stride);
   };
 
-  const int n_chunks = sl.n_chunk;
+  // split-K (gridDim.z slices, yacc != nullptr): slice z walks chunks [c_lo, c_hi) and writes
+  // its inverse-transformed partial rows to slab z of yacc (the inverse FFT is linear); the
+  // host only splits when every slice is non-empty
+  const int cps = (sl.n_chunk + (int)gridDim.z - 1) / (int)gridDim.z;
+  const int c_lo = (int)blockIdx.z * cps;
+  const int c_hi = c_lo + cps < sl.n_chunk ? c_lo + cps : sl.n_chunk;
   STAMP(0);
-  dma_half(0, 0);
-  dma_half(0, 1);
+  dma_half(c_lo * KB, 0);
+  dma_half(c_lo * KB, 1);
 
-  for (int ch = 0; ch < n_chunks; ++ch) {
+  for (int ch = c_lo; ch < c_hi; ++ch) {
     const int i0 = ch * KB;
-    const bool more = ch + 1 < n_chunks;
+    const bool more = ch + 1 < c_hi;
     const int sb = 1 + 6 * (ch & 7);
     STAMP(sb);
     wait_vmcnt<NH>();     // half 0 of this chunk landed (half 1 may still be in flight) ...
@@ -448,10 +453,33 @@ __global__ __launch_bounds__(256, 2) void bc_forward_mfma_kernel(
       float* rowp = stage + R * SROW;
       if (!ABLATE(8)) F::inverse(rowp, gl, tw, ol);
       const int64_t tok = t0 + t;
-      if (tok < n_tokens && o < n_out)
-        F::template store<XT, YF32>(rowp, gl, yv, tok * M + (int64_t)o * B, bias, (int64_t)o * B, bias_dt);
+      if (tok < n_tokens && o < n_out) {
+        if (yacc)
+          F::store_partial(rowp, gl, yacc + ((int64_t)blockIdx.z * n_tokens + tok) * M + (int64_t)o * B);
+        else
+          F::template store<XT, YF32>(rowp, gl, yv, tok * M + (int64_t)o * B, bias, (int64_t)o * B, bias_dt);
+      }
     }
     STAMP(51 + 2 * nt);
+  }
+}
+
+// split-K finish: y = slab 0 + slab 1 + ... (fixed order: bit-reproducible) with the epilogue's
+// roundings and bias (store4, the same code as the unsplit epilogue). One thread per 4 outputs;
+// M is a multiple of b >= 32.
+template <int XT, bool YF32>
+__global__ void bc_splitk_finish_kernel(const float* __restrict__ acc, int kz, int64_t n_quads, int64_t M,
+                                        const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
+  const int64_t slab = n_quads * 4;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n_quads;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e0 = q * 4;
+    float4 a = *reinterpret_cast<const float4*>(acc + e0);
+    for (int z = 1; z < kz; ++z) {
+      const float4 b = *reinterpret_cast<const float4*>(acc + z * slab + e0);
+      a = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+    }
+    store4<XT, YF32>(a, yv, e0, bias, e0 % M, bias_dt);
   }
 }
 
@@ -555,15 +583,43 @@ bool valid_dt(int d) { return d == BCFFT_F32 || d == BCFFT_F16 || d == BCFFT_BF1
 bool valid_block(int b) { return b == 32 || b == 64 || b == 128 || b == 256; }
 int promote(int a, int b) { return (b == BCFFT_NONE || a == b) ? a : BCFFT_F32; }
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+// K-slices of the MFMA kernel. One workgroup walks every chunk of 8 input blocks for its 8 tokens,
+// so a grid of fewer 8-token rows than CUs (LLaMA's down projection at prefill and decode sizes)
+// takes one whole walk regardless of N. Such grids split the chunks over kz >= 2 slices, as many
+// as fill two workgroups per CU, with >= 2 chunks per slice (each slice also pays the inverse
+// transforms and stores); no split below 4 chunks. Independent of n_out, so a fused launch
+// (q/k/v) splits exactly like its parts. kz is rounded so that no slice is empty.
+int mfma_ksplit(int64_t n, int n_in, int b) {
+  if (b > BCFFT_MFMA_MAXB || n <= 0) return 1;
+  const int n_chunks = (n_in + 7) / 8;
+  const int64_t rows = (n + 7) / 8, cus = bcfft::device_cu_count();
+  if (n_chunks < 4 || rows >= cus) return 1;
+  int64_t kz = 2 * cus / rows;
+  const int64_t kmax = (n_chunks + 1) / 2;
+  if (kz > kmax) kz = kmax;
+  if (kz < 2) kz = 2;
+  const int64_t cps = (n_chunks + kz - 1) / kz;
+  return (int)((n_chunks + cps - 1) / cps);
+}
+
 template <int B, int XT, bool YF32>
 void launch_forward(int algo, const void* x, int64_t n, int n_in, int n_out, const void* spec,
-                    const void* bias, int bias_dt, void* y, hipStream_t s) {
+                    const void* bias, int bias_dt, void* y, float* ws, hipStream_t s) {
   if constexpr (B <= BCFFT_MFMA_MAXB) {
     if (algo == BCFFT_ALGO_MFMA) {
       using G = bcfft::GeoM<B>;
-      dim3 grid((unsigned)((n + G::TT - 1) / G::TT), (unsigned)((n_out + G::OUT_PER_WG - 1) / G::OUT_PER_WG));
+      const int kz = ws ? mfma_ksplit(n, n_in, B) : 1;
+      dim3 grid((unsigned)((n + G::TT - 1) / G::TT), (unsigned)((n_out + G::OUT_PER_WG - 1) / G::OUT_PER_WG),
+                (unsigned)kz);
+      const int64_t m = (int64_t)n_out * B;
       hipLaunchKernelGGL((bcfft::bc_forward_mfma_kernel<B, XT, YF32>), grid, dim3(G::NT), 0, s, x, n,
-                         n_in, n_out, (const float2*)spec, bias, bias_dt, y);
+                         n_in, n_out, (const float2*)spec, bias, bias_dt, y, kz > 1 ? ws : nullptr);
+      if (kz > 1) {
+        const int64_t quads = n * m / 4;
+        const unsigned blocks = (unsigned)((quads + 255) / 256 < 65535 ? (quads + 255) / 256 : 65535);
+        hipLaunchKernelGGL((bcfft::bc_splitk_finish_kernel<XT, YF32>), dim3(blocks), dim3(256), 0, s,
+                           (const float*)ws, kz, quads, m, bias, bias_dt, y);
+      }
       return;
     }
   }
@@ -575,14 +631,15 @@ void launch_forward(int algo, const void* x, int64_t n, int n_in, int n_out, con
 
 template <int B>
 void launch_forward_b(int algo, int xdt, const void* x, int64_t n, int n_in, int n_out,
-                      const void* spec, const void* bias, int bias_dt, void* y, int y_dt, hipStream_t s) {
+                      const void* spec, const void* bias, int bias_dt, void* y, int y_dt, float* ws,
+                      hipStream_t s) {
   // y dtype = promote(x dtype, bias dtype): the x dtype, or fp32 for 16-bit x with another bias dtype
   const bool yf32 = y_dt == BCFFT_F32;
-  if (xdt == BCFFT_F32) launch_forward<B, BCFFT_F32, true>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, s);
-  else if (xdt == BCFFT_F16 && yf32) launch_forward<B, BCFFT_F16, true>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, s);
-  else if (xdt == BCFFT_F16) launch_forward<B, BCFFT_F16, false>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, s);
-  else if (yf32) launch_forward<B, BCFFT_BF16, true>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, s);
-  else launch_forward<B, BCFFT_BF16, false>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, s);
+  if (xdt == BCFFT_F32) launch_forward<B, BCFFT_F32, true>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, ws, s);
+  else if (xdt == BCFFT_F16 && yf32) launch_forward<B, BCFFT_F16, true>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, ws, s);
+  else if (xdt == BCFFT_F16) launch_forward<B, BCFFT_F16, false>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, ws, s);
+  else if (yf32) launch_forward<B, BCFFT_BF16, true>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, ws, s);
+  else launch_forward<B, BCFFT_BF16, false>(algo, x, n, n_in, n_out, spec, bias, bias_dt, y, ws, s);
 }
 
 template <int B>
@@ -644,9 +701,29 @@ int bcfft_spectra(const void* c, int c_dtype, int n_out_blocks, int n_in_blocks,
   return record_launch();
 }
 
-int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_features,
-                       int out_features, int block_size, const void* spectra, const void* bias,
-                       int bias_dtype, void* y, int y_dtype, int algo, void* stream) {
+// the algorithm bcfft_forward_algo runs for this geometry (AUTO resolved)
+static int resolve_algo(int algo, int n_in, int block_size) {
+  if (algo != BCFFT_ALGO_AUTO) return algo;
+  return bcfft::stat_eligible(n_in, block_size) ? BCFFT_ALGO_STAT
+                                                : (block_size <= 128 ? BCFFT_ALGO_MFMA : BCFFT_ALGO_VALU);
+}
+
+int64_t bcfft_forward_workspace_bytes(int64_t n_tokens, int in_features, int out_features, int block_size,
+                                      int algo) {
+  if (!valid_block(block_size) || n_tokens < 0 || in_features <= 0 || out_features <= 0 ||
+      in_features % block_size || out_features % block_size)
+    return -1;
+  const int n_in = in_features / block_size;
+  if (resolve_algo(algo, n_in, block_size) != BCFFT_ALGO_MFMA) return 0;
+  if (mfma_ksplit(n_tokens, n_in, block_size) < 2) return 0;
+  const int kz = mfma_ksplit(n_tokens, n_in, block_size);
+  return kz * n_tokens * (int64_t)out_features * (int64_t)sizeof(float);   // one fp32 slab per slice
+}
+
+int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_features,
+                     int out_features, int block_size, const void* spectra, const void* bias,
+                     int bias_dtype, void* y, int y_dtype, int algo, void* workspace,
+                     int64_t workspace_bytes, void* stream) {
   if (!valid_block(block_size)) return BCFFT_ERR_BLOCK;
   if (n_tokens < 0 || in_features <= 0 || out_features <= 0 || in_features % block_size ||
       out_features % block_size)
@@ -660,12 +737,16 @@ int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_feat
     return BCFFT_ERR_ARG;
   if (n_tokens == 0) return BCFFT_OK;
   if (!x || !y || !spectra) return BCFFT_ERR_ARG;
-  if (!aligned16(x) || !aligned16(y) || !aligned16(spectra) || (bias && !aligned16(bias))) return BCFFT_ERR_ALIGN;
+  if (!aligned16(x) || !aligned16(y) || !aligned16(spectra) || (bias && !aligned16(bias)) ||
+      (workspace && !aligned16(workspace)))
+    return BCFFT_ERR_ALIGN;
   const int n_in = in_features / block_size, n_out = out_features / block_size;
   const bool stat_ok = bcfft::stat_eligible(n_in, block_size);
   if (algo == BCFFT_ALGO_STAT && !stat_ok) return BCFFT_ERR_BLOCK;
-  if (algo == BCFFT_ALGO_AUTO)
-    algo = stat_ok ? BCFFT_ALGO_STAT : (block_size <= 128 ? BCFFT_ALGO_MFMA : BCFFT_ALGO_VALU);
+  algo = resolve_algo(algo, n_in, block_size);
+  // the workspace is used only when it is as large as bcfft_forward_workspace_bytes asks
+  const int64_t need = bcfft_forward_workspace_bytes(n_tokens, in_features, out_features, block_size, algo);
+  float* ws = (workspace && need > 0 && workspace_bytes >= need) ? (float*)workspace : nullptr;
   hipStream_t s = (hipStream_t)stream;
   if (algo == BCFFT_ALGO_STAT) {
     bcfft::launch_forward_stat(block_size, n_in, x_dtype, y_dtype == BCFFT_F32, x, n_tokens, n_out,
@@ -673,12 +754,19 @@ int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_feat
     return record_launch();
   }
   switch (block_size) {
-    case 32: launch_forward_b<32>(algo, x_dtype, x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, y_dtype, s); break;
-    case 64: launch_forward_b<64>(algo, x_dtype, x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, y_dtype, s); break;
-    case 128: launch_forward_b<128>(algo, x_dtype, x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, y_dtype, s); break;
-    default: launch_forward_b<256>(algo, x_dtype, x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, y_dtype, s); break;
+    case 32: launch_forward_b<32>(algo, x_dtype, x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, y_dtype, ws, s); break;
+    case 64: launch_forward_b<64>(algo, x_dtype, x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, y_dtype, ws, s); break;
+    case 128: launch_forward_b<128>(algo, x_dtype, x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, y_dtype, ws, s); break;
+    default: launch_forward_b<256>(algo, x_dtype, x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, y_dtype, ws, s); break;
   }
   return record_launch();
+}
+
+int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_features,
+                       int out_features, int block_size, const void* spectra, const void* bias,
+                       int bias_dtype, void* y, int y_dtype, int algo, void* stream) {
+  return bcfft_forward_ws(x, x_dtype, n_tokens, in_features, out_features, block_size, spectra, bias,
+                          bias_dtype, y, y_dtype, algo, nullptr, 0, stream);
 }
 
 int bcfft_forward_glu(const void* x, int x_dtype, int64_t n_tokens, int in_features, int gate_features,

@@ -1071,6 +1071,10 @@ int cu_count() {
   return g_cu_count;
 }
 
+}  // namespace
+int bcfft::device_cu_count() { return cu_count(); }
+namespace {
+
 template <int B, int KS, int XT, bool YF32, bool GLU = false>
 void launch_stat(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt,
                  void* y, hipStream_t s) {

@@ -118,3 +118,31 @@ def test_gfx950_code_object_has_no_packed_fp32(built_lib, tmp_path):
     assert re.search(r"v_pk_(add|mul|fma)_f32", asm) is None
     assert "v_mfma_f32_16x16x32_bf16" in asm
     assert "global_load_lds_dword" in asm
+
+
+def test_forward_workspace_bytes_without_gpu(built_lib):
+    """Split-K workspace sizing is host logic: non-zero only where the MFMA kernel runs a grid of
+    fewer 8-token rows than CUs over >= 4 chunks of 8 input blocks (no GPU here: 256 CUs)."""
+    from bcfft import _lib
+    lib = _lib.load()
+    ws = lib.bcfft_forward_workspace_bytes
+    AUTO, MFMA, VALU, STAT = (_lib.ALGOS[a] for a in ("auto", "mfma", "valu", "stationary"))
+    assert ws(100, 11008, 4096, 128, AUTO) == 6 * 100 * 4096 * 4       # 13 rows: 6 slices of 2 chunks
+    assert ws(20, 11008, 4096, 128, AUTO) == 6 * 20 * 4096 * 4         # decode batch
+    assert ws(1024, 11008, 4096, 128, AUTO) == 4 * 1024 * 4096 * 4     # 128 rows: 4 slices (3,3,3,2)
+    assert ws(1700, 11008, 4096, 128, AUTO) == 2 * 1700 * 4096 * 4     # prefill batch: 2 slices
+    assert ws(2040, 11008, 4096, 128, AUTO) == 2 * 2040 * 4096 * 4     # 255 rows < 256 CUs
+    assert ws(2048, 11008, 4096, 128, AUTO) == 0                    # 256 rows: full grid
+    assert ws(100, 4096, 4096, 128, AUTO) == 0                      # stationary
+    assert ws(100, 4096, 4096, 128, MFMA) == 2 * 100 * 4096 * 4        # forced MFMA: 4 chunks
+    assert ws(100, 3072, 4096, 128, MFMA) == 0                      # 3 chunks: never split
+    assert ws(100, 11008, 4096, 128, VALU) == 0
+    assert ws(100, 4096, 4096, 256, AUTO) == 0                      # b = 256: VALU kernel
+    assert ws(100, 4000, 4096, 128, AUTO) == -1
+    assert ws(0, 11008, 4096, 128, AUTO) == 0
+    fake = 4096
+    F32, NONE = _lib.BCFFT_F32, _lib.BCFFT_NONE
+    fw = lib.bcfft_forward_ws
+    assert fw(fake, F32, 8, 11008, 4096, 128, fake, None, NONE, fake, F32, AUTO, fake + 4, 1 << 20, None) == 4
+    assert fw(None, F32, 0, 11008, 4096, 128, None, None, NONE, None, F32, AUTO, None, 0, None) == 0
+    assert fw(fake, F32, 8, 4096, 4096, 128, fake, None, NONE, fake, F32, 9, None, 0, None) == 6
