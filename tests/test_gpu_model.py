@@ -38,21 +38,23 @@ def test_inference_mode_patched_llama():
     assert gen.shape == (2, 15)
 
 
-def test_model_bench_small_llama():
+@pytest.mark.parametrize("targets", ["all", "mlp"])
+def test_model_bench_small_llama(targets):
     pytest.importorskip("transformers")
     assert torch.cuda.is_available()
     import model_bench as MB
     line = MB.main(["--layers", "2", "--prompts", "6", "--max-len", "40", "--batch-size", "3",
-                    "--runs", "1", "--warmup", "1", "--new-tokens", "4",
+                    "--runs", "1", "--warmup", "1", "--new-tokens", "4", "--targets", targets,
                     "--config-overrides",
                     '{"hidden_size": 1024, "intermediate_size": 2816, "num_attention_heads": 8, '
                     '"num_key_value_heads": 8, "vocab_size": 512}'])
     cfg = line["config"]
-    assert cfg["fused_qkv_layers"] == 2 and cfg["fused_gate_up_layers"] == 2
+    assert cfg["fused_qkv_layers"] == (2 if targets == "all" else 0) and cfg["fused_gate_up_layers"] == 2
     assert line["value"] > 0 and line["decode_new_tokens_per_s"] > 0
     par = line["projection_parity_layer0"]
-    want = {"self_attn.q_proj", "self_attn.k_proj", "self_attn.v_proj", "self_attn.o_proj",
-            "mlp.down_proj", "mlp.gate_up_swiglu(fused)"}
+    want = {"mlp.down_proj", "mlp.gate_up_swiglu(fused)"}
+    if targets == "all":
+        want |= {"self_attn.q_proj", "self_attn.k_proj", "self_attn.v_proj", "self_attn.o_proj"}
     assert want <= set(par), par
     for name, r in par.items():
         # bf16 outputs: one rounding alone is ~1e-3 rms relative vs fp32 (the fused SwiGLU has
