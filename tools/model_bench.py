@@ -202,6 +202,8 @@ def main(argv=None):
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
+    if args.prompts < world:
+        raise SystemExit(f"--prompts {args.prompts} < {world} ranks: every rank needs a prompt")
     model = build_model(args, dev)
     cfg = model.config
     prompts = E.synthetic_prompts(args.prompts, args.max_len, cfg.vocab_size, seed=args.seed)
