@@ -211,7 +211,11 @@ class BlockCirculantLinear(nn.Module):
         # same error as the reference's reshape (:246) for a 2D input of the wrong width
         x_flat.reshape(x_flat.shape[0], self.in_blocks, self.block_size)
         _lib.require_device(x_flat, "BlockCirculantLinear.forward")
-        y_flat = _BCFunction.apply(x_flat, self.c, self.bias, self)
+        if torch.is_grad_enabled() and (x_flat.requires_grad or self.c.requires_grad or
+                                        (self.bias is not None and self.bias.requires_grad)):
+            y_flat = _BCFunction.apply(x_flat, self.c, self.bias, self)
+        else:                    # no graph to record (eval, no_grad, inference_mode): skip autograd
+            y_flat = _ops.forward(x_flat, self._spectra(self.c), self.bias, self.block_size, self.out_features)
         if is_3d:
             return y_flat.view(bs, sl, self.out_features)                                      # :273-274
         return y_flat
