@@ -45,13 +45,15 @@ def test_model_bench_small_llama(targets):
     import model_bench as MB
     line = MB.main(["--layers", "2", "--prompts", "6", "--max-len", "40", "--batch-size", "3",
                     "--runs", "1", "--warmup", "1", "--new-tokens", "4", "--targets", targets,
+                    "--block-sizes", "64,128",
                     "--config-overrides",
                     '{"hidden_size": 1024, "intermediate_size": 2816, "num_attention_heads": 8, '
                     '"num_key_value_heads": 8, "vocab_size": 512}'])
     cfg = line["config"]
+    assert cfg["block_size"] == 128 and cfg["patched_layers"] == 2
     assert cfg["fused_qkv_layers"] == (2 if targets == "all" else 0) and cfg["fused_gate_up_layers"] == 2
     assert line["value"] > 0 and line["decode_new_tokens_per_s"] > 0
-    par = line["projection_parity_layer0"]
+    par = line["projection_parity_first_patched_layer"]
     want = {"mlp.down_proj", "mlp.gate_up_swiglu(fused)"}
     if targets == "all":
         want |= {"self_attn.q_proj", "self_attn.k_proj", "self_attn.v_proj", "self_attn.o_proj"}
@@ -63,3 +65,18 @@ def test_model_bench_small_llama(targets):
         assert r["rel_err"] < 5e-3, (name, r)
     for k in ("last_kl", "last_cos", "last_top1_acc", "last_topk_overlap"):
         assert k in line["teacher_student"]
+
+
+def test_model_bench_last_k_layers():
+    """--num-layers / --patch-position (the reference patcher's first/last k): the last layer only."""
+    pytest.importorskip("transformers")
+    import model_bench as MB
+    line = MB.main(["--layers", "3", "--prompts", "4", "--max-len", "24", "--batch-size", "2",
+                    "--runs", "1", "--warmup", "0", "--new-tokens", "0", "--num-layers", "1",
+                    "--patch-position", "last", "--config-overrides",
+                    '{"hidden_size": 1024, "intermediate_size": 2816, "num_attention_heads": 8, '
+                    '"num_key_value_heads": 8, "vocab_size": 512}'])
+    cfg = line["config"]
+    assert cfg["patched_layers"] == 1 and cfg["fused_qkv_layers"] == 1 and cfg["fused_gate_up_layers"] == 1
+    for name, r in line["projection_parity_first_patched_layer"].items():
+        assert r["rel_err_vs_rounded"] < 1e-3, (name, r)

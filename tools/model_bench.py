@@ -175,8 +175,10 @@ def projection_parity(model, layer_idx, batch):
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--layers", type=int, default=32)
-    ap.add_argument("--block-size", type=int, default=128)
+    ap.add_argument("--layers", type=int, default=32, help="decoder layers of the model")
+    ap.add_argument("--block-sizes", default="128", help="comma list, as bench_all_in_one's --block_sizes")
+    ap.add_argument("--num-layers", type=int, default=-1, help="layers to patch (-1: all)")
+    ap.add_argument("--patch-position", default="first", choices=["first", "last"])
     ap.add_argument("--targets", default="all", choices=["all", "mlp"])
     ap.add_argument("--prompts", type=int, default=100, help="prompts over all ranks (prompts_100.txt: 99)")
     ap.add_argument("--max-len", type=int, default=128)
@@ -184,12 +186,13 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--runs", type=int, default=3)
     ap.add_argument("--new-tokens", type=int, default=32, help="greedy decode length (0: skip)")
-    ap.add_argument("--dense", type=int, default=1, help="also time the dense (teacher) model")
+    ap.add_argument("--dense", type=int, default=1, help="also time the dense (teacher) model's decode")
     ap.add_argument("--topk", type=int, default=5)
     ap.add_argument("--temperature", type=float, default=1.0)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--config-overrides", default="{}", help="JSON LlamaConfig overrides (tests)")
     args = ap.parse_args(argv)
+    block_sizes = [int(b) for b in args.block_sizes.split(",") if b.strip()]
 
     import patch_llama_fft as P
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -214,75 +217,81 @@ def main(argv=None):
     if world > 1:
         dist.all_reduce(tok)
     total_tokens = int(tok.item())
+    n_patch = cfg.num_hidden_layers if args.num_layers < 0 else args.num_layers
+    patched = P._layer_indices(cfg.num_hidden_layers, n_patch, args.patch_position)
 
-    res = {}
     teacher_last, t_dense = prefill(model, batches, args.warmup, args.runs)
-    res["dense_prefill_s"] = t_dense
-    if args.dense and args.new_tokens:
-        res["dense_decode_s"] = decode(model, batches, args.new_tokens, cfg.pad_token_id)
+    dense_decode_s = decode(model, batches, args.new_tokens, cfg.pad_token_id) if args.dense and args.new_tokens else None
 
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    patch = P.patch_linear_with_block_circulant if args.targets == "all" else P.patch_mlp_with_block_circulant
-    import contextlib
-    import io
-    with contextlib.redirect_stdout(io.StringIO()):             # the patcher logs every projection
-        patch(model, num_layers_to_patch=cfg.num_hidden_layers, block_size=args.block_size,
-              patch_position="first")
-    n_qkv = P.fuse_attention_qkv(model)
-    n_glu = P.fuse_mlp_gate_up(model)
-    torch.cuda.synchronize()
-    res["patch_s"] = time.perf_counter() - t0
-    torch.cuda.empty_cache()
+    line = None
+    for bi, b in enumerate(block_sizes):
+        if bi > 0:                      # patching is in place: rebuild the same seeded dense model
+            del model
+            torch.cuda.empty_cache()
+            model = build_model(args, dev)
+        res = {}
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        patch = P.patch_linear_with_block_circulant if args.targets == "all" else P.patch_mlp_with_block_circulant
+        import contextlib
+        import io
+        with contextlib.redirect_stdout(io.StringIO()):         # the patcher logs every projection
+            patch(model, num_layers_to_patch=n_patch, block_size=b, patch_position=args.patch_position)
+        n_qkv = P.fuse_attention_qkv(model)
+        n_glu = P.fuse_mlp_gate_up(model)
+        torch.cuda.synchronize()
+        res["patch_s"] = time.perf_counter() - t0
+        torch.cuda.empty_cache()
 
-    student_last, t_bc = prefill(model, batches, args.warmup, args.runs)
-    metrics = E.last_token_metrics(student_last, teacher_last, args.temperature, args.topk)
-    parity = projection_parity(model, 0, batches[0])
-    if args.new_tokens:
-        res["bc_decode_s"] = decode(model, batches, args.new_tokens, cfg.pad_token_id)
+        student_last, t_bc = prefill(model, batches, args.warmup, args.runs)
+        metrics = E.last_token_metrics(student_last, teacher_last, args.temperature, args.topk)
+        parity = projection_parity(model, patched[0], batches[0]) if patched else {}
+        if args.new_tokens:
+            res["bc_decode_s"] = decode(model, batches, args.new_tokens, cfg.pad_token_id)
 
-    # config 5's single collective: every rank's last-token logits to every rank (RCCL). The
-    # prompt shards are shard_bounds' contiguous slices, so gather_rows reassembles them in order.
-    if world > 1:
-        from bcfft.shard import gather_rows
-        barrier()
-        tg = time.perf_counter()
-        rows = gather_rows(student_last.contiguous(), args.prompts)
-        barrier()
-        res["allgather_logits_s"] = sync_max(time.perf_counter() - tg)
-        assert rows.shape[0] == args.prompts
+        # config 5's single collective: every rank's last-token logits to every rank (RCCL). The
+        # prompt shards are shard_bounds' contiguous slices, so gather_rows reassembles them in order.
+        if world > 1:
+            from bcfft.shard import gather_rows
+            barrier()
+            tg = time.perf_counter()
+            rows = gather_rows(student_last.contiguous(), args.prompts)
+            barrier()
+            res["allgather_logits_s"] = sync_max(time.perf_counter() - tg)
+            assert rows.shape[0] == args.prompts
 
-    if rank == 0:
-        n_prompts_new = args.prompts * args.new_tokens
-        line = {
-            "metric": "BC-patched LLaMA-2-7B prefill tokens/s (all linear layers BC)",
-            "value": round(total_tokens / t_bc, 1), "unit": "tokens/s", "n_gpus": world,
-            "higher_is_better": True, "scaling": "weak" if world == 1 else "strong",
-            "data": "synthetic prompts (seeded ids, lengths U[max_len/4, max_len]); random-init "
-                    "LLaMA-2-7B architecture, bf16 (no weights/tokenizer offline)",
-            "config": {"layers": cfg.num_hidden_layers, "hidden": cfg.hidden_size,
-                       "intermediate": cfg.intermediate_size, "vocab": cfg.vocab_size,
-                       "block_size": args.block_size, "targets": args.targets,
-                       "prompts": args.prompts, "max_len": args.max_len,
-                       "batch_size": args.batch_size, "tokens": total_tokens,
-                       "fused_qkv_layers": n_qkv, "fused_gate_up_layers": n_glu,
-                       "parallelism": f"prompt-replicas x{world}"},
-            "prefill_ms": round(t_bc * 1e3, 3),
-            "dense_prefill_ms": round(t_dense * 1e3, 3),
-            "dense_prefill_tokens_per_s": round(total_tokens / t_dense, 1),
-            "bc_vs_dense_prefill": round(t_dense / t_bc, 3),
-            "patch_s": round(res["patch_s"], 3),
-            "teacher_student": metrics,
-            "projection_parity_layer0": parity,
-        }
-        if "bc_decode_s" in res:
-            line["decode_new_tokens_per_s"] = round(n_prompts_new / res["bc_decode_s"], 1)
-        if "dense_decode_s" in res:
-            line["dense_decode_new_tokens_per_s"] = round(n_prompts_new / res["dense_decode_s"], 1)
-        if "allgather_logits_s" in res:
-            line["allgather_logits_ms"] = round(res["allgather_logits_s"] * 1e3, 3)
-            line["value_with_allgather"] = round(total_tokens / (t_bc + res["allgather_logits_s"]), 1)
-        print(json.dumps(line), flush=True)
+        if rank == 0:
+            n_prompts_new = args.prompts * args.new_tokens
+            line = {
+                "metric": "BC-patched LLaMA-2-7B prefill tokens/s",
+                "value": round(total_tokens / t_bc, 1), "unit": "tokens/s", "n_gpus": world,
+                "higher_is_better": True, "scaling": "weak" if world == 1 else "strong",
+                "data": "synthetic prompts (seeded ids, lengths U[max_len/4, max_len]); random-init "
+                        "LLaMA-2-7B architecture, bf16 (no weights/tokenizer offline)",
+                "config": {"layers": cfg.num_hidden_layers, "hidden": cfg.hidden_size,
+                           "intermediate": cfg.intermediate_size, "vocab": cfg.vocab_size,
+                           "block_size": b, "targets": args.targets, "patched_layers": len(patched),
+                           "patch_position": args.patch_position,
+                           "prompts": args.prompts, "max_len": args.max_len,
+                           "batch_size": args.batch_size, "tokens": total_tokens,
+                           "fused_qkv_layers": n_qkv, "fused_gate_up_layers": n_glu,
+                           "parallelism": f"prompt-replicas x{world}"},
+                "prefill_ms": round(t_bc * 1e3, 3),
+                "dense_prefill_ms": round(t_dense * 1e3, 3),
+                "dense_prefill_tokens_per_s": round(total_tokens / t_dense, 1),
+                "bc_vs_dense_prefill": round(t_dense / t_bc, 3),
+                "patch_s": round(res["patch_s"], 3),
+                "teacher_student": metrics,
+                "projection_parity_first_patched_layer": parity,
+            }
+            if "bc_decode_s" in res:
+                line["decode_new_tokens_per_s"] = round(n_prompts_new / res["bc_decode_s"], 1)
+            if dense_decode_s:
+                line["dense_decode_new_tokens_per_s"] = round(n_prompts_new / dense_decode_s, 1)
+            if "allgather_logits_s" in res:
+                line["allgather_logits_ms"] = round(res["allgather_logits_s"] * 1e3, 3)
+                line["value_with_allgather"] = round(total_tokens / (t_bc + res["allgather_logits_s"]), 1)
+            print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return line if rank == 0 else None
