@@ -101,8 +101,9 @@ int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_feat
                        int bias_dtype, void* y, int y_dtype, int algo, void* stream);
 
 /* Optional workspace of bcfft_forward_ws, in bytes (0: the forward never uses one; < 0:
- * invalid geometry). Non-zero only where the split-bf16 MFMA kernel (algo, AUTO resolved) runs a
- * grid shorter than the device's CU count (n_tokens < 8 x CUs) over >= 32 input blocks, e.g.
+ * invalid geometry). Non-zero only where the split-bf16 MFMA kernel or the VALU kernel (algo,
+ * AUTO resolved) runs a grid too short to fill the device (MFMA: n_tokens < 8 x CUs) over >= 4
+ * chunks of input blocks, e.g.
  * LLaMA's 11008 -> 4096 down projection at prefill and decode sizes: it then splits the input
  * blocks over kz >= 2 workgroup slices (as many as fill two workgroups per CU, >= 2 chunks of 8
  * input blocks each) that write fp32 partial outputs to the workspace (kz x n_tokens x

@@ -61,7 +61,7 @@ template <int B, int XT, bool YF32>
 __global__ __launch_bounds__(512) void bc_forward_valu_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_in, int n_out,
     const float2* __restrict__ spec, const void* __restrict__ bias, int bias_dt,
-    void* __restrict__ yv) {
+    void* __restrict__ yv, float* __restrict__ yacc) {
   using G = GeoV<B>;
   using F = Fft<B>;
   constexpr int H = G::H, L = G::L, TT = G::TT, IC = G::IC, SROW = G::SROW, XROW = G::XROW;
@@ -132,11 +132,16 @@ __global__ __launch_bounds__(512) void bc_forward_valu_kernel(
       }
   };
 
+  // split-K (gridDim.z slices, yacc != nullptr): as in bc_forward_mfma_kernel, slice z walks
+  // chunks [c_lo, c_hi) and writes its partial rows to slab z of yacc
   const int n_chunks = (n_in + IC - 1) / IC;
-  load_chunk(0);
+  const int cps = (n_chunks + (int)gridDim.z - 1) / (int)gridDim.z;
+  const int c_lo = (int)blockIdx.z * cps;
+  const int c_hi = c_lo + cps < n_chunks ? c_lo + cps : n_chunks;
+  load_chunk(c_lo * IC);
   __syncthreads();
 
-  for (int ch = 0; ch < n_chunks; ++ch) {
+  for (int ch = c_lo; ch < c_hi; ++ch) {
     const int i0 = ch * IC;
     __syncthreads();
     store_chunk();
@@ -153,7 +158,7 @@ __global__ __launch_bounds__(512) void bc_forward_valu_kernel(
         *reinterpret_cast<float2*>(xdst + k * XROW) = F::untangle(row, k, tw);
       }
     }
-    if (ch + 1 < n_chunks) load_chunk(i0 + IC);
+    if (ch + 1 < c_hi) load_chunk(i0 + IC);
     __syncthreads();
 
     if (wave_active) {
@@ -219,8 +224,12 @@ __global__ __launch_bounds__(512) void bc_forward_valu_kernel(
       float* row = stage + R * SROW;
       F::inverse(row, gl, tw, 0);
       const int64_t tok = t0 + t;
-      if (tok < n_tokens && o < n_out)
-        F::template store<XT, YF32>(row, gl, yv, tok * M + (int64_t)o * B, bias, (int64_t)o * B, bias_dt);
+      if (tok < n_tokens && o < n_out) {
+        if (yacc)
+          F::store_partial(row, gl, yacc + ((int64_t)blockIdx.z * n_tokens + tok) * M + (int64_t)o * B);
+        else
+          F::template store<XT, YF32>(row, gl, yv, tok * M + (int64_t)o * B, bias, (int64_t)o * B, bias_dt);
+      }
     }
   }
 }
@@ -589,17 +598,36 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 // as fill two workgroups per CU, with >= 2 chunks per slice (each slice also pays the inverse
 // transforms and stores); no split below 4 chunks. Independent of n_out, so a fused launch
 // (q/k/v) splits exactly like its parts. kz is rounded so that no slice is empty.
-int mfma_ksplit(int64_t n, int n_in, int b) {
-  if (b > BCFFT_MFMA_MAXB || n <= 0) return 1;
-  const int n_chunks = (n_in + 7) / 8;
-  const int64_t rows = (n + 7) / 8, cus = bcfft::device_cu_count();
-  if (n_chunks < 4 || rows >= cus) return 1;
-  int64_t kz = 2 * cus / rows;
+// rows = workgroup rows of the unsplit grid, slots = resident workgroups per CU
+int ksplit_rows(int64_t rows, int n_chunks, int slots) {
+  const int64_t cus = bcfft::device_cu_count();
+  if (n_chunks < 4 || rows >= cus || 2 * rows > slots * cus) return 1;
+  int64_t kz = slots * cus / rows;
   const int64_t kmax = (n_chunks + 1) / 2;
   if (kz > kmax) kz = kmax;
   if (kz < 2) kz = 2;
   const int64_t cps = (n_chunks + kz - 1) / kz;
   return (int)((n_chunks + cps - 1) / cps);
+}
+int mfma_ksplit(int64_t n, int n_in, int b) {
+  if (b > BCFFT_MFMA_MAXB || n <= 0) return 1;
+  return ksplit_rows((n + 7) / 8, (n_in + 7) / 8, 2);
+}
+// the VALU kernel: 16-token rows, chunks of 64 / L input blocks (bcfft::GeoV<B>::IC); its LDS
+// allows two workgroups per CU at b = 128, one at b = 64 and 256 (b = 32 is counted as one)
+int valu_ksplit(int64_t n, int n_in, int b) {
+  if (n <= 0) return 1;
+  const int ic = 512 / (b / 2 <= 32 ? 4 : 8) / 16;
+  return ksplit_rows((n + 15) / 16, (n_in + ic - 1) / ic, b == 128 ? 2 : 1);
+}
+
+template <int XT, bool YF32>
+void launch_finish(const float* ws, int kz, int64_t n, int64_t m, const void* bias, int bias_dt, void* y,
+                   hipStream_t s) {
+  const int64_t quads = n * m / 4;
+  const unsigned blocks = (unsigned)((quads + 255) / 256 < 65535 ? (quads + 255) / 256 : 65535);
+  hipLaunchKernelGGL((bcfft::bc_splitk_finish_kernel<XT, YF32>), dim3(blocks), dim3(256), 0, s, ws, kz, quads,
+                     m, bias, bias_dt, y);
 }
 
 template <int B, int XT, bool YF32>
@@ -614,19 +642,18 @@ void launch_forward(int algo, const void* x, int64_t n, int n_in, int n_out, con
       const int64_t m = (int64_t)n_out * B;
       hipLaunchKernelGGL((bcfft::bc_forward_mfma_kernel<B, XT, YF32>), grid, dim3(G::NT), 0, s, x, n,
                          n_in, n_out, (const float2*)spec, bias, bias_dt, y, kz > 1 ? ws : nullptr);
-      if (kz > 1) {
-        const int64_t quads = n * m / 4;
-        const unsigned blocks = (unsigned)((quads + 255) / 256 < 65535 ? (quads + 255) / 256 : 65535);
-        hipLaunchKernelGGL((bcfft::bc_splitk_finish_kernel<XT, YF32>), dim3(blocks), dim3(256), 0, s,
-                           (const float*)ws, kz, quads, m, bias, bias_dt, y);
-      }
+      if (kz > 1) launch_finish<XT, YF32>(ws, kz, n, m, bias, bias_dt, y, s);
       return;
     }
   }
   using G = bcfft::GeoV<B>;
-  dim3 grid((unsigned)((n + G::TT - 1) / G::TT), (unsigned)((n_out + G::OUT_PER_WG - 1) / G::OUT_PER_WG));
+  static_assert(G::IC == 512 / (B / 2 <= 32 ? 4 : 8) / 16, "valu_ksplit's chunk size");
+  const int kz = ws ? valu_ksplit(n, n_in, B) : 1;
+  dim3 grid((unsigned)((n + G::TT - 1) / G::TT), (unsigned)((n_out + G::OUT_PER_WG - 1) / G::OUT_PER_WG),
+            (unsigned)kz);
   hipLaunchKernelGGL((bcfft::bc_forward_valu_kernel<B, XT, YF32>), grid, dim3(G::NT), 0, s, x, n, n_in,
-                     n_out, (const float2*)spec, bias, bias_dt, y);
+                     n_out, (const float2*)spec, bias, bias_dt, y, kz > 1 ? ws : nullptr);
+  if (kz > 1) launch_finish<XT, YF32>(ws, kz, n, (int64_t)n_out * B, bias, bias_dt, y, s);
 }
 
 template <int B>
@@ -714,9 +741,11 @@ int64_t bcfft_forward_workspace_bytes(int64_t n_tokens, int in_features, int out
       in_features % block_size || out_features % block_size)
     return -1;
   const int n_in = in_features / block_size;
-  if (resolve_algo(algo, n_in, block_size) != BCFFT_ALGO_MFMA) return 0;
-  if (mfma_ksplit(n_tokens, n_in, block_size) < 2) return 0;
-  const int kz = mfma_ksplit(n_tokens, n_in, block_size);
+  const int a = resolve_algo(algo, n_in, block_size);
+  int kz = 1;
+  if (a == BCFFT_ALGO_MFMA && block_size <= BCFFT_MFMA_MAXB) kz = mfma_ksplit(n_tokens, n_in, block_size);
+  else if (a == BCFFT_ALGO_VALU || a == BCFFT_ALGO_MFMA) kz = valu_ksplit(n_tokens, n_in, block_size);
+  if (kz < 2) return 0;
   return kz * n_tokens * (int64_t)out_features * (int64_t)sizeof(float);   // one fp32 slab per slice
 }
 

@@ -230,11 +230,14 @@ def test_backward_vs_dense(dev):
 
 # ------------------------------------------------- split-K MFMA launches (short grids, K >= 32 blocks)
 SPLIT_CASES = [
-    # (K, M, b, N, x dtype, bias dtype or None)
-    (11008, 4096, 128, 1700, "bfloat16", None),        # LLaMA down projection, prefill batch
-    (11008, 4096, 128, 3, "float32", "float32"),       # 6 slices of 2 chunks (decode-size N)
-    (4224, 640, 128, 37, "bfloat16", "float32"),       # 5 chunks: slices of 2 + 2 + 1, fp32 promotion
-    (1024, 512, 32, 61, "float16", "float16"),         # b = 32: exactly 4 chunks
+    # (K, M, b, N, x dtype, bias dtype or None, algo)
+    (11008, 4096, 128, 1700, "bfloat16", None, "auto"),       # LLaMA down projection, prefill batch
+    (11008, 4096, 128, 3, "float32", "float32", "auto"),      # 6 slices of 2 chunks (decode-size N)
+    (4224, 640, 128, 37, "bfloat16", "float32", "auto"),      # 5 chunks: slices of 2 + 2 + 1, fp32 promotion
+    (1024, 512, 32, 61, "float16", "float16", "auto"),        # b = 32: exactly 4 chunks
+    (4096, 4096, 256, 20, "bfloat16", None, "auto"),          # VALU kernel, b = 256: 4 chunks, 2 slices
+    (11008, 4096, 256, 37, "float32", "float32", "auto"),     # VALU b = 256: 11 chunks, 6 slices
+    (11008, 4096, 128, 50, "float32", "bfloat16", "valu"),    # VALU b = 128: 22 chunks, 11 slices
 ]
 
 
@@ -246,26 +249,26 @@ def _split_inputs(k, m, b, n, xdt, bdt, dev):
     return c, bv, x
 
 
-@pytest.mark.parametrize("k,m,b,n,xdt,bdt", SPLIT_CASES)
-def test_split_k_vs_oracle_and_unsplit(dev, k, m, b, n, xdt, bdt):
+@pytest.mark.parametrize("k,m,b,n,xdt,bdt,algo", SPLIT_CASES)
+def test_split_k_vs_oracle_and_unsplit(dev, k, m, b, n, xdt, bdt, algo):
     """The split path (workspace from ops.forward) vs the oracle, bit-reproducible run to run, and
     within fp32 summation-order noise of the unsplit launch (bcfft_forward_algo, no workspace)."""
     from bcfft import _lib, ops
     c, bv, x = _split_inputs(k, m, b, n, xdt, bdt, dev)
     lib = _lib.load()
-    wsb = lib.bcfft_forward_workspace_bytes(n, k, m, b, _lib.ALGOS["auto"])
+    wsb = lib.bcfft_forward_workspace_bytes(n, k, m, b, _lib.ALGOS[algo])
     assert wsb > 0 and wsb % (n * m * 4) == 0 and wsb // (n * m * 4) >= 2
     spec = ops.spectra(torch.from_numpy(c).to(dev))
     xt = _to_dev(x, xdt, dev)
     bt = None if bdt is None else torch.from_numpy(bv).to(dev).to(getattr(torch, bdt))
-    y1 = ops.forward(xt, spec, bt, b, m, algo="auto")
-    y2 = ops.forward(xt, spec, bt, b, m, algo="auto")
+    y1 = ops.forward(xt, spec, bt, b, m, algo=algo)
+    y2 = ops.forward(xt, spec, bt, b, m, algo=algo)
     assert torch.equal(y1, y2)
     y0 = torch.empty_like(y1)
     _lib.check(lib.bcfft_forward_algo(xt.data_ptr(), _lib.dtype_code(xt.dtype), n, k, m, b, spec.data_ptr(),
                                       0 if bt is None else bt.data_ptr(),
                                       _lib.BCFFT_NONE if bt is None else _lib.dtype_code(bt.dtype),
-                                      y0.data_ptr(), _lib.dtype_code(y0.dtype), _lib.ALGOS["auto"],
+                                      y0.data_ptr(), _lib.dtype_code(y0.dtype), _lib.ALGOS[algo],
                                       _lib.stream_handle(xt.device)), "unsplit")
     rel = ((y1.float() - y0.float()).norm() / y0.float().norm()).item()
     # 16-bit x: the epilogue rounds to x's dtype before the bias, so order noise can flip roundings
