@@ -598,12 +598,14 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 // as fill two workgroups per CU, with >= 2 chunks per slice (each slice also pays the inverse
 // transforms and stores); no split below 4 chunks. Independent of n_out, so a fused launch
 // (q/k/v) splits exactly like its parts. kz is rounded so that no slice is empty.
-// rows = workgroup rows of the unsplit grid, slots = resident workgroups per CU
-int ksplit_rows(int64_t rows, int n_chunks, int slots) {
+// rows = workgroup rows of the unsplit grid, slots = resident workgroups per CU, min_chunks =
+// chunks per slice at least (a slice also pays the inverse transforms and stores: 2 measured
+// best for the MFMA kernel, 1 for the VALU kernel; profiles/r01_splitk_timing.jsonl)
+int ksplit_rows(int64_t rows, int n_chunks, int slots, int min_chunks) {
   const int64_t cus = bcfft::device_cu_count();
   if (n_chunks < 4 || rows >= cus || 2 * rows > slots * cus) return 1;
   int64_t kz = slots * cus / rows;
-  const int64_t kmax = (n_chunks + 1) / 2;
+  const int64_t kmax = (n_chunks + min_chunks - 1) / min_chunks;
   if (kz > kmax) kz = kmax;
   if (kz < 2) kz = 2;
   const int64_t cps = (n_chunks + kz - 1) / kz;
@@ -611,14 +613,14 @@ int ksplit_rows(int64_t rows, int n_chunks, int slots) {
 }
 int mfma_ksplit(int64_t n, int n_in, int b) {
   if (b > BCFFT_MFMA_MAXB || n <= 0) return 1;
-  return ksplit_rows((n + 7) / 8, (n_in + 7) / 8, 2);
+  return ksplit_rows((n + 7) / 8, (n_in + 7) / 8, 2, 2);
 }
 // the VALU kernel: 16-token rows, chunks of 64 / L input blocks (bcfft::GeoV<B>::IC); its LDS
 // allows two workgroups per CU at b = 128, one at b = 64 and 256 (b = 32 is counted as one)
 int valu_ksplit(int64_t n, int n_in, int b) {
   if (n <= 0) return 1;
   const int ic = 512 / (b / 2 <= 32 ? 4 : 8) / 16;
-  return ksplit_rows((n + 15) / 16, (n_in + ic - 1) / ic, b == 128 ? 2 : 1);
+  return ksplit_rows((n + 15) / 16, (n_in + ic - 1) / ic, b == 128 ? 2 : 1, 1);
 }
 
 template <int XT, bool YF32>

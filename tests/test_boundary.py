@@ -136,9 +136,9 @@ def test_forward_workspace_bytes_without_gpu(built_lib):
     assert ws(100, 4096, 4096, 128, AUTO) == 0                      # stationary
     assert ws(100, 4096, 4096, 128, MFMA) == 2 * 100 * 4096 * 4        # forced MFMA: 4 chunks
     assert ws(100, 3072, 4096, 128, MFMA) == 0                      # 3 chunks: never split
-    assert ws(50, 11008, 4096, 128, VALU) == 11 * 50 * 4096 * 4     # VALU b = 128: 22 chunks of 4 blocks
-    assert ws(20, 4096, 4096, 256, AUTO) == 2 * 20 * 4096 * 4       # VALU b = 256: 4 chunks
-    assert ws(37, 11008, 4096, 256, AUTO) == 6 * 37 * 4096 * 4      # VALU b = 256: 11 chunks
+    assert ws(50, 11008, 4096, 128, VALU) == 22 * 50 * 4096 * 4     # VALU b = 128: 22 chunks of 4 blocks
+    assert ws(20, 4096, 4096, 256, AUTO) == 4 * 20 * 4096 * 4       # VALU b = 256: 4 chunks, 1 per slice
+    assert ws(37, 11008, 4096, 256, AUTO) == 11 * 37 * 4096 * 4     # VALU b = 256: 11 chunks
     assert ws(2048, 4096, 4096, 256, AUTO) == 2 * 2048 * 4096 * 4   # 128 rows, 1 workgroup per CU: 2 slices
     assert ws(4096, 4096, 4096, 256, AUTO) == 0                     # 256 rows: full grid
     assert ws(100, 3072, 4096, 256, AUTO) == 0                      # 12 blocks: 3 chunks

@@ -235,9 +235,10 @@ SPLIT_CASES = [
     (11008, 4096, 128, 3, "float32", "float32", "auto"),      # 6 slices of 2 chunks (decode-size N)
     (4224, 640, 128, 37, "bfloat16", "float32", "auto"),      # 5 chunks: slices of 2 + 2 + 1, fp32 promotion
     (1024, 512, 32, 61, "float16", "float16", "auto"),        # b = 32: exactly 4 chunks
-    (4096, 4096, 256, 20, "bfloat16", None, "auto"),          # VALU kernel, b = 256: 4 chunks, 2 slices
-    (11008, 4096, 256, 37, "float32", "float32", "auto"),     # VALU b = 256: 11 chunks, 6 slices
-    (11008, 4096, 128, 50, "float32", "bfloat16", "valu"),    # VALU b = 128: 22 chunks, 11 slices
+    (4096, 4096, 256, 20, "bfloat16", None, "auto"),          # VALU kernel, b = 256: 4 chunks, 4 slices
+    (11008, 4096, 256, 37, "float32", "float32", "auto"),     # VALU b = 256: 11 chunks, 11 slices
+    (4096, 4096, 256, 1500, "float32", None, "auto"),         # VALU b = 256: 94 rows, 2 slices of 2
+    (11008, 4096, 128, 50, "float32", "bfloat16", "valu"),    # VALU b = 128: 22 chunks, 22 slices
 ]
 
 
