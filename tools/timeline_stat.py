@@ -6,7 +6,8 @@ the STAMP points of bc_forward_stat_kernel (bcfft_stat.hip):
   0 start | per M-tile it (base 1 + 7 min(it, 7)): +0 loop top, +1 inverse done, +2 stores and
   next DMA issued, +3 forward done, +4 after barrier Ba, +5 MFMAs + Y written, +6 after Bb | 63 end
 and the phase switches (outputs are WRONG when set) time what each phase costs.
-usage: python tools/timeline_stat.py [K M B IO N]
+usage: python tools/timeline_stat.py [K M B IO N]   (GLU=1: the fused gate/up + SwiGLU launch,
+       M = gate features, same weights for gate and up)
 """
 import ctypes
 import os
@@ -37,28 +38,34 @@ def run(k, m, b, io, n):
     lib.bcfft_set_ablation_stat.argtypes = [ctypes.c_int]
     torch.manual_seed(0)
     c = (torch.randn(m // b, k // b, b) * 0.01).cuda()
-    spec = ops.spectra(c)
+    glu = os.environ.get("GLU", "0") == "1"
+    spec = ops.spectra(ops.glu_weights(c, c) if glu else c)
     x = torch.randn(n, k, device="cuda").to(dt)
+
+    def fwd():
+        if glu:
+            return ops.forward_glu(x, spec, b, m)
+        return ops.forward(x, spec, None, b, m, algo="stationary")
 
     def timeit(iters=30):
         for _ in range(3):
-            ops.forward(x, spec, None, b, m, algo="stationary")
+            fwd()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         s.record()
         for _ in range(iters):
-            ops.forward(x, spec, None, b, m, algo="stationary")
+            fwd()
         e.record()
         torch.cuda.synchronize()
         return s.elapsed_time(e) / iters * 1e3
 
-    groups = -(-(m // b) // 32)
+    groups = -(-(m // b) // (16 if glu else 32))
     buf = torch.zeros(256 * groups * 8 * 64, dtype=torch.int64, device="cuda")
 
     def stamps():
         buf.zero_()
         _lib.check(lib.bcfft_set_stamps_stat(buf.data_ptr()), "stamps")
-        ops.forward(x, spec, None, b, m, algo="stationary")
+        fwd()
         torch.cuda.synchronize()
         _lib.check(lib.bcfft_set_stamps_stat(None), "stamps")
         st = buf.view(-1, 64).cpu().numpy().astype(np.int64)
