@@ -613,7 +613,10 @@ int ksplit_rows(int64_t rows, int n_chunks, int slots, int min_chunks) {
 }
 int mfma_ksplit(int64_t n, int n_in, int b) {
   if (b > BCFFT_MFMA_MAXB || n <= 0) return 1;
-  return ksplit_rows((n + 7) / 8, (n_in + 7) / 8, 2, 2);
+  // one chunk per slice pays at decode sizes (<= 4 rows: 24.0 vs 27.7 us at N = 20), two above
+  // (35.1 vs 37.3 us at N = 256)
+  const int64_t rows = (n + 7) / 8;
+  return ksplit_rows(rows, (n_in + 7) / 8, 2, rows <= 4 ? 1 : 2);
 }
 // the VALU kernel: 16-token rows, chunks of 64 / L input blocks (bcfft::GeoV<B>::IC); its LDS
 // allows two workgroups per CU at b = 128, one at b = 64 and 256 (b = 32 is counted as one)

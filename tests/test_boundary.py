@@ -128,7 +128,8 @@ def test_forward_workspace_bytes_without_gpu(built_lib):
     ws = lib.bcfft_forward_workspace_bytes
     AUTO, MFMA, VALU, STAT = (_lib.ALGOS[a] for a in ("auto", "mfma", "valu", "stationary"))
     assert ws(100, 11008, 4096, 128, AUTO) == 6 * 100 * 4096 * 4       # 13 rows: 6 slices of 2 chunks
-    assert ws(20, 11008, 4096, 128, AUTO) == 6 * 20 * 4096 * 4         # decode batch
+    assert ws(20, 11008, 4096, 128, AUTO) == 11 * 20 * 4096 * 4        # decode batch: 1 chunk per slice
+    assert ws(40, 11008, 4096, 128, AUTO) == 6 * 40 * 4096 * 4         # 5 rows: 2 chunks per slice
     assert ws(1024, 11008, 4096, 128, AUTO) == 4 * 1024 * 4096 * 4     # 128 rows: 4 slices (3,3,3,2)
     assert ws(1700, 11008, 4096, 128, AUTO) == 2 * 1700 * 4096 * 4     # prefill batch: 2 slices
     assert ws(2040, 11008, 4096, 128, AUTO) == 2 * 2040 * 4096 * 4     # 255 rows < 256 CUs

@@ -232,7 +232,8 @@ def test_backward_vs_dense(dev):
 SPLIT_CASES = [
     # (K, M, b, N, x dtype, bias dtype or None, algo)
     (11008, 4096, 128, 1700, "bfloat16", None, "auto"),       # LLaMA down projection, prefill batch
-    (11008, 4096, 128, 3, "float32", "float32", "auto"),      # 6 slices of 2 chunks (decode-size N)
+    (11008, 4096, 128, 3, "float32", "float32", "auto"),      # 11 slices of 1 chunk (decode-size N)
+    (11008, 4096, 128, 40, "bfloat16", "bfloat16", "auto"),   # 6 slices of 2 chunks
     (4224, 640, 128, 37, "bfloat16", "float32", "auto"),      # 5 chunks: slices of 2 + 2 + 1, fp32 promotion
     (1024, 512, 32, 61, "float16", "float16", "auto"),        # b = 32: exactly 4 chunks
     (4096, 4096, 256, 20, "bfloat16", None, "auto"),          # VALU kernel, b = 256: 4 chunks, 4 slices
