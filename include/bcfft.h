@@ -11,7 +11,9 @@
  *  - Plain pointers and sizes only; every buffer is caller-owned device memory (torch's
  *    allocator in the Python layer). No entry point allocates, frees or synchronises.
  *  - `stream` is a hipStream_t passed as void* (NULL = legacy default stream). Work is
- *    enqueued asynchronously; entry points are reentrant and keep no mutable global state.
+ *    enqueued asynchronously; entry points are reentrant. The only global state is a per-device
+ *    cache of the CU count (atomic slots, filled on first use per device ordinal), which sizes
+ *    persistent grids and split-K workspaces for the CURRENT device.
  *  - Return value: BCFFT_OK (0) or a BCFFT_ERR_* status. Shape/dtype/alignment problems are
  *    reported before anything is launched. bcfft_status_string() gives a message.
  *  - dtype codes: BCFFT_F32, BCFFT_F16, BCFFT_BF16 (BCFFT_NONE for "no bias").

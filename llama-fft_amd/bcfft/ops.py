@@ -40,6 +40,17 @@ def spectra(c: torch.Tensor, transpose_conj: bool = False) -> torch.Tensor:
     return out
 
 
+def _check_spectra(spec: torch.Tensor, n_out: int, n_in: int, b: int, what: str) -> None:
+    """The library cannot see the spectra buffer's size: a buffer built for another geometry
+    would be read out of bounds. Checked here, before the launch."""
+    if b <= 0 or n_out <= 0 or n_in <= 0:
+        raise ValueError(f"{what}: invalid geometry (out_blocks={n_out}, in_blocks={n_in}, block_size={b})")
+    need = _lib.load().bcfft_spectra_bytes(n_out, n_in, b)
+    if need < 0 or spec.dtype != torch.float32 or spec.numel() * 4 < need:
+        raise ValueError(f"{what}: spectra buffer of {spec.numel() * spec.element_size()} B "
+                         f"({spec.dtype}) does not hold the ({n_out}, {n_in}, {b}) operator ({need} B)")
+
+
 def glu_weights(c_gate: torch.Tensor, c_up: torch.Tensor) -> torch.Tensor:
     """Interleave gate/up circulant columns (nO, nI, b) into the (32 G, nI, b) weight of
     bcfft_forward_glu, G = ceil(nO / 16): group g = gate blocks [16g, 16g+16) then up blocks
@@ -63,6 +74,9 @@ def forward_glu(x2d: torch.Tensor, spec_gu: torch.Tensor, block_size: int, gate_
     spectra(glu_weights(c_gate, c_up)). h has x2d's dtype."""
     _lib.require_device(x2d, "bcfft.forward_glu")
     n, k = x2d.shape
+    if block_size > 0 and gate_features % block_size == 0 and k % block_size == 0:
+        _check_spectra(spec_gu, 32 * (-(-(gate_features // block_size) // 16)), k // block_size, block_size,
+                       "bcfft.forward_glu")
     x2d = x2d.contiguous()
     if x2d.data_ptr() % 16:
         x2d = x2d.clone()
@@ -99,6 +113,8 @@ def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, bl
     "valu" (exact fp32 MAC). See include/bcfft.h."""
     _lib.require_device(x2d, "bcfft.forward")
     n, k = x2d.shape
+    if block_size > 0 and out_features % block_size == 0 and k % block_size == 0:
+        _check_spectra(spec, out_features // block_size, k // block_size, block_size, "bcfft.forward")
     x2d = x2d.contiguous()
     if x2d.data_ptr() % 16:
         x2d = x2d.clone()

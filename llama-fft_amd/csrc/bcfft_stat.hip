@@ -35,6 +35,8 @@
 // DESIGN.md has the layouts, swizzles and the roofline accounting.
 #include "bcfft_device.h"
 
+#include <atomic>
+
 namespace bcfft {
 
 typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
@@ -1058,17 +1060,23 @@ __global__ void bc_stat_image_kernel(int n_out, int n_in, float2* __restrict__ s
 }  // namespace bcfft
 
 namespace {
-int g_cu_count = 0;
+// CU count of the CURRENT device, cached per device ordinal. Atomic slots: concurrent first
+// calls from several threads race only to store the same value (a device's CU count does not
+// change), so grid and workspace sizing stay consistent for every caller.
+constexpr int kMaxDevices = 64;
+std::atomic<int> g_cu_count[kMaxDevices];
 int cu_count() {
-  if (g_cu_count <= 0) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-      g_cu_count = n;
-    else
-      g_cu_count = 256;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  if (dev >= 0 && dev < kMaxDevices) {
+    const int c = g_cu_count[dev].load(std::memory_order_relaxed);
+    if (c > 0) return c;
   }
-  return g_cu_count;
+  int n = 0;
+  if (dev < 0 || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+    n = 256;
+  if (dev >= 0 && dev < kMaxDevices) g_cu_count[dev].store(n, std::memory_order_relaxed);
+  return n;
 }
 
 }  // namespace

@@ -120,11 +120,15 @@ class _BCFunction(torch.autograd.Function):
         m = ctx.module
         dx = dc = dbias = None
         dy = dy.contiguous()
+        # The reference adds the bias AFTER y.to(x.dtype) (:266-271): with a 16-bit x and a wider
+        # bias, autograd hands the add's x-side input its gradient rounded to x.dtype, and the
+        # .to() backward widens it again. dx and dc see that rounded dy; dbias sees dy itself.
+        dy_x = dy.to(x2d.dtype) if (bias is not None and dy.dtype != x2d.dtype) else dy
         if ctx.needs_input_grad[0]:
             spec_t = m._spectra(c, adjoint=True)
-            dx = _ops.forward(dy, spec_t, None, m.block_size, m.in_features).to(x2d.dtype)
+            dx = _ops.forward(dy_x, spec_t, None, m.block_size, m.in_features).to(x2d.dtype)
         if ctx.needs_input_grad[1]:
-            dc = _ops.grad_c(x2d, dy, m.block_size, c.dtype)
+            dc = _ops.grad_c(x2d, dy_x, m.block_size, c.dtype)
         if bias is not None and ctx.needs_input_grad[2]:
             dbias = dy.sum(dim=0).to(bias.dtype)
         return dx, dc, dbias, None
@@ -197,19 +201,26 @@ class BlockCirculantLinear(nn.Module):
         self._spec_cache = {}
         return super()._apply(fn, *args, **kwargs)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def _flatten(self, x: torch.Tensor) -> torch.Tensor:
+        """x -> (N, in_features) with the reference's errors: ValueError for other ranks
+        (:238-239), AssertionError for a 3D input of the wrong width (:230), the reshape's
+        RuntimeError (:246) for a 2D one."""
         if x.dim() == 3:                                                                       # :228-233
             bs, sl, in_f = x.shape
             assert in_f == self.in_features
             x_flat = x.reshape(bs * sl, in_f)
-            is_3d = True
         elif x.dim() == 2:                                                                     # :234-238
             x_flat = x
-            is_3d = False
         else:
             raise ValueError("Unsupported input dim")                                          # :239
-        # same error as the reference's reshape (:246) for a 2D input of the wrong width
         x_flat.reshape(x_flat.shape[0], self.in_blocks, self.block_size)
+        return x_flat
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x_flat = self._flatten(x)
+        is_3d = x.dim() == 3
+        if is_3d:
+            bs, sl = x.shape[0], x.shape[1]
         _lib.require_device(x_flat, "BlockCirculantLinear.forward")
         if torch.is_grad_enabled() and (x_flat.requires_grad or self.c.requires_grad or
                                         (self.bias is not None and self.bias.requires_grad)):
@@ -375,7 +386,7 @@ class BCFusedGateUp(nn.Module):
         if not self._fused_ok(x):
             return torch.nn.functional.silu(self._gate(x)) * self._up(x)
         shape = x.shape
-        x2d = x.reshape(-1, shape[-1])
+        x2d = self._gate._flatten(x)                   # the module's rank / width errors
         h = _ops.forward_glu(x2d, self._spectra(), self._gate.block_size, self._gate.out_features)
         return h.view(*shape[:-1], self._gate.out_features)
 
@@ -438,7 +449,11 @@ class BCFusedProjections:
         return x.is_cuda and not grad and (all(biases) or not any(biases))
 
     def _weights(self):
-        key = tuple((m.c.data_ptr(), _version_of(m.c)) for m in self.mods) + (self.mods[0].c.device,)
+        # the bias is part of the key: bias-only updates (train_bias, a checkpoint that changes
+        # only the bias) must reach the fused launch as they reach the modules' own forward
+        key = tuple((m.c.data_ptr(), _version_of(m.c),
+                     None if m.bias is None else (m.bias.data_ptr(), _version_of(m.bias)))
+                    for m in self.mods) + (self.mods[0].c.device,)
         if key != self._key:
             self._spec = _ops.spectra(torch.cat([m.c.detach() for m in self.mods], dim=0))
             self._bias = (None if self.mods[0].bias is None
@@ -454,9 +469,7 @@ class BCFusedProjections:
         if not (self._x is x and self._ver == ver and idx in self._left):
             spec, bias = self._weights()
             shape = x.shape
-            if x.dim() not in (2, 3):
-                raise ValueError("Unsupported input dim")                              # :239
-            x2d = x.reshape(-1, shape[-1])
+            x2d = m._flatten(x)                         # the module's rank / width errors
             y = _ops.forward(x2d, spec, bias, m.block_size, sum(self.splits))
             outs, o = [], 0
             for n in self.splits:

@@ -30,9 +30,15 @@ def main():
         ("bwd_4096sq_b128", 4096, 4096, 128, (3,), "fp32", "fp32", True),        # north-star shape
         ("bwd_256x256_b32_bf16", 256, 256, 32, (9,), "bf16", "bf16", True),      # module.to(bf16)
         ("bwd_512x1024_b256_f16x", 512, 1024, 256, (4,), "fp16", "fp32", False),
+        # 16-bit x, fp32 module with a bias: y = y16 + bias promotes to fp32, and autograd rounds
+        # the x-side gradient to bf16 before dx / dc (patch_llama_fft.py:266-271)
+        ("bwd_promote_bf16x_f32bias_512x256_b64", 512, 256, 64, (7,), "bf16", "fp32", True),
     ]
+    only = os.environ.get("GOLDEN_ONLY")          # regenerate selected fixtures only
     print("backward cases:")
     for i, (name, k, m, b, pre, xdt, mdt, bias) in enumerate(cases):
+        if only and name not in only.split(","):
+            continue
         torch.manual_seed(4000 + i)
         mod = plf.BlockCirculantLinear(k, m, block_size=b, bias=bias)
         with torch.no_grad():
@@ -49,6 +55,8 @@ def main():
               dbias=grads[2] if bias else None, block_size=b, x_dtype=xdt, mod_dtype=mdt)
 
     print("from_linear cases:")
+    if only:
+        return
     for i, (m, k, b, d, scale) in enumerate([(256, 512, 64, "bf16", 1.0),
                                              (512, 1024, 128, "fp16", 0.02)]):
         torch.manual_seed(5000 + i)

@@ -151,3 +151,28 @@ def test_fused_qkv_matches_unfused(dev):
         assert a.shape == b.shape and torch.equal(a, b)
     assert ((out - ref).norm() / ref.norm()).item() < 1e-6
 
+
+
+def test_fused_routes_check_width_and_see_bias_updates(dev):
+    """The fused q/k/v and gate/up routes raise the module's errors for a wrong-width input, and
+    a bias-only update reaches the fused q/k/v launch."""
+    import patch_llama_fft as P
+    torch.manual_seed(3)
+    mods = [P.BlockCirculantLinear(4096, m, block_size=128, bias=True).to(dev).eval() for m in (4096, 1024, 1024)]
+    fused = P.BCFusedProjections(mods)
+    x = torch.randn(2, 5, 4096, device=dev)
+    with torch.no_grad():
+        y0 = fused.output(0, x).clone()
+        for i in (1, 2):
+            fused.output(i, x)
+        with pytest.raises(AssertionError):
+            fused.output(0, torch.randn(2, 5, 2048, device=dev))
+        with pytest.raises(RuntimeError):
+            fused.output(0, torch.randn(10, 2048, device=dev))
+        mods[0].bias.add_(1.0)                      # bias-only update
+        y1 = fused.output(0, x)
+        assert torch.allclose(y1, y0 + 1.0, rtol=1e-5, atol=1e-4)
+        g = P.BlockCirculantLinear(4096, 4096, block_size=128, bias=False).to(dev).eval()
+        u = P.BlockCirculantLinear(4096, 4096, block_size=128, bias=False).to(dev).eval()
+        with pytest.raises(AssertionError):
+            P.BCFusedGateUp(g, u)(torch.randn(1, 3, 2048, device=dev))

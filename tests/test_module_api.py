@@ -164,3 +164,29 @@ def test_fuse_attention_qkv_rewires_without_new_parameters():
     with pytest.raises(RuntimeError, match="ROCm device"):   # no CPU path behind the fused route
         model.model.layers[0].self_attn.q_proj(torch.zeros(2, 256))
 
+
+
+def test_flatten_reference_errors(plf):
+    """The module's (and the fused routes') input checks raise the reference's exceptions:
+    AssertionError for a 3D input of the wrong width (:230), the reshape's RuntimeError for a 2D
+    one (:246), ValueError for other ranks (:239)."""
+    m = plf.BlockCirculantLinear(256, 128, block_size=64)
+    assert m._flatten(torch.zeros(2, 3, 256)).shape == (6, 256)
+    with pytest.raises(AssertionError):
+        m._flatten(torch.zeros(2, 3, 192))
+    with pytest.raises(RuntimeError):
+        m._flatten(torch.zeros(5, 192))
+    with pytest.raises(ValueError, match="Unsupported input dim"):
+        m._flatten(torch.zeros(1, 2, 3, 256))
+
+
+def test_spectra_buffer_size_is_checked():
+    """ops.forward / forward_glu refuse a spectra buffer built for a smaller operator before
+    anything reaches the library (which cannot see the buffer's size)."""
+    from bcfft import ops
+    ok = torch.empty(ops.spectra_numel(32, 32, 128), dtype=torch.float32)
+    ops._check_spectra(ok, 32, 32, 128, "t")
+    with pytest.raises(ValueError, match="does not hold"):
+        ops._check_spectra(ok, 86, 32, 128, "t")
+    with pytest.raises(ValueError, match="does not hold"):
+        ops._check_spectra(ok.to(torch.float16), 32, 32, 128, "t")
