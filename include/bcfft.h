@@ -43,8 +43,12 @@ enum bcfft_dtype { BCFFT_NONE = -1, BCFFT_F32 = 0, BCFFT_F16 = 1, BCFFT_BF16 = 2
  *  MFMA: per-bin complex MAC on the matrix cores as a bf16 GEMM with hi/lo splitting of both
  *        operands ((Xhi+Xlo)(Chi+Clo), fp32 accumulate; ~1e-5 relative). block_size <= 128.
  *  VALU: per-bin complex MAC in fp32 FMAs (the reference's fp32 arithmetic). Any block size.
+ *  DFT:  the STAT weights, with the forward and inverse DFTs of the blocks also on the matrix
+ *        cores (dense fp16 GEMMs against a 2^-7-scaled DFT table, even/odd split) instead of
+ *        VALU FFTs; ~3.5e-4 relative. Geometry: block_size 128 with in_features 4096.
  *  AUTO: STAT where eligible, else MFMA for block_size <= 128, else VALU. */
-enum bcfft_algo { BCFFT_ALGO_AUTO = 0, BCFFT_ALGO_MFMA = 1, BCFFT_ALGO_VALU = 2, BCFFT_ALGO_STAT = 3 };
+enum bcfft_algo { BCFFT_ALGO_AUTO = 0, BCFFT_ALGO_MFMA = 1, BCFFT_ALGO_VALU = 2, BCFFT_ALGO_STAT = 3,
+                  BCFFT_ALGO_DFT = 4 };
 
 enum bcfft_status {
   BCFFT_OK = 0,

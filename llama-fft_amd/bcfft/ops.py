@@ -97,7 +97,7 @@ def glu_eligible(in_features: int, block_size: int) -> bool:
 
 
 def default_algo() -> str:
-    """BCFFT_ALGO env var: auto (default) | stationary | mfma | valu."""
+    """BCFFT_ALGO env var: auto (default) | dft | stationary | mfma | valu."""
     import os
     a = os.environ.get("BCFFT_ALGO", "auto").lower()
     if a not in _lib.ALGOS:

@@ -86,6 +86,50 @@ __device__ __forceinline__ void split_bf16(float2 v, uint32_t& hi, uint32_t& lo)
   lo = __builtin_bit_cast(uint32_t, l);
 }
 
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_t;
+// ------------------------------------------------------------------ cross-lane / scaling helpers
+// (stationary and DFT-on-MFMA kernels)
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+constexpr int DPP_XOR1 = 0xB1;   // quad_perm [1,0,3,2]
+constexpr int DPP_XOR2 = 0x4E;   // quad_perm [2,3,0,1]
+constexpr int DPP_XOR3 = 0x1B;   // quad_perm [3,2,1,0]
+constexpr int DPP_P0 = 0xB4;     // quad_perm [0,1,3,2]
+
+// v_mov through inline asm: the compiler cannot hoist or CSE what depends on it, so per-lane
+// addresses are rematerialised inside each phase instead of being kept (and spilled) across the
+// persistent loop next to the 128 VGPRs of stationary weights
+__device__ __forceinline__ int opaque(int v) {
+  int r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+
+// packed fp16 product of two fp16 pairs (v_pk_mul_f16)
+__device__ __forceinline__ uint32_t pkmul(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2_t, a) * __builtin_bit_cast(f16x2_t, b));
+}
+
+// max over the wave's 64 lanes, uniform: quad and row by DPP, the four rows by readlane
+__device__ __forceinline__ float wave_max(float v) {
+  v = fmaxf(v, dpp<DPP_XOR1>(v));
+  v = fmaxf(v, dpp<DPP_XOR2>(v));
+  v = fmaxf(v, dpp<0x141>(v));                     // row_half_mirror
+  v = fmaxf(v, dpp<0x140>(v));                     // row_mirror
+  const int u = __float_as_int(v);
+  const float a = fmaxf(__int_as_float(__builtin_amdgcn_readlane(u, 0)), __int_as_float(__builtin_amdgcn_readlane(u, 16)));
+  const float b = fmaxf(__int_as_float(__builtin_amdgcn_readlane(u, 32)), __int_as_float(__builtin_amdgcn_readlane(u, 48)));
+  return fmaxf(a, b);
+}
+
+// scale exponent for fp16 hi/lo: 2^nsc mx < 2^15, clamped so 2^nsc and 2^-nsc stay normal
+__device__ __forceinline__ int stat_scale_exp(float mx) {
+  const int nsc = 15 - __builtin_amdgcn_frexp_expf(mx);
+  return nsc < -126 ? -126 : (nsc > 126 ? 126 : nsc);
+}
+
 // ------------------------------------------------------------------ LDS-DMA (inline asm)
 // hipcc neither counts an asm load in its s_waitcnt bookkeeping nor drains it at a barrier, so
 // the x stream stays in flight across compute phases; every wait on it is explicit below.
@@ -457,6 +501,10 @@ bool launch_forward_stat(int b, int n_in, int xdt, bool yf32, const void* x, int
 bool launch_forward_glu(int b, int n_in, int xdt, const void* x, int64_t n, int n_gate, const void* spec,
                         void* h, hipStream_t s);
 void launch_stat_image(int b, int n_out, int n_in, void* spec, hipStream_t s);
+// DFT-on-MFMA kernel (bcfft_dm.hip): the STAT image's geometry subset b = 128, K = 4096
+bool dm_eligible(int n_in, int b);
+bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, const void* x, int64_t n, int n_out,
+                       const void* spec, const void* bias, int bias_dt, void* y, hipStream_t s);
 
 // weight prep (bcfft_prep.hip): loss-aware circulant projection of a dense (n_out*b, n_in*b)
 // weight into c (n_out, n_in, b) fp32; false for an unsupported block size

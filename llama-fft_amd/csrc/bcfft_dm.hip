@@ -1,0 +1,481 @@
+// bcfft_dm.hip — block-circulant forward with all three stages on the matrix cores (gfx950).
+//
+// Same operator as bc_forward_stat_kernel (BlockCirculantLinear.forward,
+// patch_llama_fft.py:226-275) and the same stationary weights: one persistent 512-thread
+// workgroup per CU keeps its output group's conj(C) s_C spectra (the STAT image, fp16 B
+// fragments) in 128 VGPRs per lane and streams tokens in tiles of 4. What changes is the
+// transforms: the real DFT of every 128-point x row and the inverse DFT of every output row are
+// dense fp16 GEMMs on v_mfma_f32_16x16x32_f16 instead of VALU FFTs.
+//
+//  * Even/odd split (half of a 128 x 128 DFT): a_t = x_t + x_{t+64}, d_t = x_t - x_{t+64}
+//    (t < 64). The even packed bins are a 64-point real DFT of a, the odd ones the DFT of d
+//    against e^{-2 pi i (2j+1) t / 128}: X = [a Fe | d Fo] with two 64 x 64 matrices (the fp16
+//    table bcfft_dm_table.h, times 2^-7). The inverse is the transpose: E = Fe Y_even,
+//    O = Fo Y_odd, y_t = E_t + O_t, y_{t+64} = E_t - O_t; its weights (1/b, 2/b) are the bin-0
+//    factor 1/2 in the MAC and the per-token output scale.
+//  * Wave roles per M-tile: waves 0-3 (F) transform token w's x rows (stage 1) while waves 4-7
+//    (I) inverse-transform token w-4 of the previous tile (stage 3) and stream the next x in by
+//    LDS-DMA; then all 8 waves run the per-bin complex MAC (stage 2) on their 8 bins, exactly as
+//    the stationary kernel. Two workgroup barriers per M-tile, two 64 KiB LDS regions.
+//  * Numerics: a, d split into fp16 hi + lo under a per-(token, 16-block half) power-of-two
+//    scale; X split into hi + lo; C and the table one fp16 term each; Y one fp16 term (a fixed
+//    2^-21 keeps it in range); fp32 accumulation everywhere: ~3.5e-4 relative on the layer
+//    output (tests/dm_model.py restates it; north star: 1e-3).
+//
+// Geometry: b = 128 with K = 4096 (32 input blocks: two K-steps of 16), any M (output groups of
+// 32 blocks), x fp32 / fp16 / bf16, y = promote(x, bias). LDS and register maps below; every
+// LDS access pattern is checked conflict-free by tools/lds_banks_dm.py.
+#include "bcfft_device.h"
+#include "bcfft_dm_table.h"
+
+namespace bcfft {
+
+namespace dmk {
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+
+constexpr int B = 128, NI = 32, KS = 2, NOG = 32, TT = 4, NW = 8;
+constexpr int BW = 8, NT = 2;                       // bins per wave, 16-wide N-tiles per group
+constexpr int K = NI * B;
+constexpr int SLOT = 16384;                         // one token of a tile
+constexpr int REGION = TT * SLOT;                   // 64 KiB
+constexpr int F_OFF = 2 * REGION;                   // DFT table image, 64 rows x 256 B
+constexpr int SC_OFF = F_OFF + 16384;               // scale exponents [2 parity][4 token][2 half]
+constexpr int LDS_BYTES = SC_OFF + 64;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+
+// F image: row t, 16-B chunk ch stored at chunk ch ^ fsw(t) (conflict-free for the stage-3 row
+// reads and the stage-1 transposed reads)
+__device__ __forceinline__ int fsw(int t) { return ((t & 3) << 1) | (t & 8); }
+// X unit (16 B = 4 input blocks x (re, im) fp16 of bin f, precision p, block quad q) of the
+// token in slot tok, K-step ks; swizzle: the precision bit flips with bin bit 2, the quad with
+// the token pair
+__device__ __forceinline__ int xunit(int ks, int f, int p, int q, int tok) {
+  return ks * 8192 + 128 * f + 16 * ((4 * (p ^ ((f >> 2) & 1))) + (q ^ (3 * (tok >> 1))));
+}
+// Y unit (16 B = 4 bins of parity par of wave w x (re, im) fp16) of output block o; lies over
+// the K-step-0 X units of wave w's bins in the same token slot
+__device__ __forceinline__ int yunit(int w, int o, int par) { return w * 1024 + 16 * (32 * par + o); }
+
+__device__ __forceinline__ uint32_t pk_rtz(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b));
+}
+__device__ __forceinline__ uint32_t pk_rne(float a, float b) {
+  const f16x2 h = {(_Float16)a, (_Float16)b};
+  return __builtin_bit_cast(uint32_t, h);
+}
+__device__ __forceinline__ float lo16(uint32_t p) { return (float)__builtin_bit_cast(f16x2, p).x; }
+__device__ __forceinline__ float hi16(uint32_t p) { return (float)__builtin_bit_cast(f16x2, p).y; }
+// (a, b) -> fp16 hi (toward zero) and lo = the rest (toward zero)
+__device__ __forceinline__ void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
+  hi = pk_rtz(a, b);
+  lo = pk_rtz(a - lo16(hi), b - hi16(hi));
+}
+__device__ __forceinline__ f16x8 frag(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return __builtin_bit_cast(f16x8, make_uint4(a, b, c, d));
+}
+}  // namespace dmk
+
+template <int XT, bool YF32>
+__global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
+    const void* __restrict__ xv, int64_t n_tokens, int n_out, const uint32_t* __restrict__ stat,
+    const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
+  using namespace dmk;
+  constexpr int ES = XTraits<XT>::ES;
+  constexpr bool Y32 = YF32 || XT == BCFFT_F32;
+  constexpr int ESY = Y32 ? 4 : 2;
+  constexpr int NPIECE = BW * KS * NT;
+  constexpr int XOFF = ES == 4 ? 0 : 8192;          // x rows within a token slot
+  constexpr int NDMA = K * ES / 1024;               // 1-KiB LDS-DMA pieces per token
+
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  int* wsc = reinterpret_cast<int*>(lds + SC_OFF);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool fwave = wave < 4;                      // F waves: stage 1 of token slot `wave`
+  const int tslot = wave & 3;                       // I waves: stage 3 of token slot wave - 4
+  const int n_groups = (n_out + NOG - 1) / NOG;
+  const int grp_o = blockIdx.x % n_groups;
+  const int wg_in_grp = blockIdx.x / n_groups;
+  const int64_t M = (int64_t)n_out * B;
+  const int64_t n_mtiles = (n_tokens + TT - 1) / TT;
+  const int gstride = (gridDim.x - grp_o + n_groups - 1) / n_groups;
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+
+  // ---- x of one token -> its slot by LDS-DMA (I waves; the buffer range zero-fills tokens past
+  // n_tokens). LDS is lane-linear per piece, so the slot's unit swizzle (logical 16-B unit u of
+  // block row r at physical u ^ (r & 15)) is applied to the global source offsets.
+  auto dma_token = [&](int64_t m, char* region) {
+    const int64_t tok = m * TT + tslot;
+    const bool ok = tok < n_tokens;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>((const char*)xv) + (ok ? tok : 0) * K * ES, 0, ok ? K * ES : 0, 0x00020000);
+    const int dl = opaque(lane);
+    const uint32_t dst0 = lds_base + (uint32_t)(region - lds) + tslot * SLOT + XOFF;
+    if constexpr (ES == 4) {                        // piece q: rows 2q + (lane >> 5), 512 B each
+      int vb[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const int h = dl >> 5;
+        vb[c] = h * 512 + 16 * ((dl & 31) ^ ((2 * c + h) & 15));
+      }
+#pragma unroll
+      for (int q = 0; q < NDMA; ++q) {
+        uint32_t keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(vb[q & 7]), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
+      }
+    } else {                                        // piece q: rows 4q + (lane >> 4), 256 B each
+      int vb[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int r = dl >> 4;
+        vb[c] = r * 256 + 16 * ((dl & 15) ^ ((4 * c + r) & 15));
+      }
+#pragma unroll
+      for (int q = 0; q < NDMA; ++q) {
+        uint32_t keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(vb[q & 3]), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
+      }
+    }
+  };
+
+  // ---- prologue: first tile's x (I waves), the DFT table, the stationary B fragments
+  if (!fwave && wg_in_grp < n_mtiles) dma_token(wg_in_grp, lds);
+  {
+    const uint4* tab = reinterpret_cast<const uint4*>(kDmF);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int c = tid + 512 * r;                  // chunk c: row c >> 4, chunk c & 15
+      const int t = c >> 4, ch = c & 15;
+      *reinterpret_cast<uint4*>(lds + F_OFF + 256 * t + 16 * (ch ^ fsw(t))) = tab[c];
+    }
+  }
+  const float inv_sc = __uint_as_float(stat[1]);
+  f16x8 creg[BW][KS][NT];
+  {
+    const uint4* img = reinterpret_cast<const uint4*>(stat + 4) + ((int64_t)(grp_o * NW + wave) * NPIECE) * 64 + lane;
+#pragma unroll
+    for (int fb = 0; fb < BW; ++fb)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          creg[fb][ks][nt] = __builtin_bit_cast(f16x8, img[((fb * KS + ks) * NT + nt) * 64]);
+  }
+  wait_vmcnt<0>();
+  lds_barrier();
+
+  // ---- stage 1 (F wave, token slot s = wave): x rows -> X hi/lo units, in place, per half
+  auto stage1 = [&](char* region, int par) {
+    const int l = opaque(lane);
+    const int b16 = l & 15, g = l >> 4;
+    char* slot = region + wave * SLOT;
+    // transposed-read lane address of the table: row 8g + q (+ 32 ks + 4 sec), chunk
+    // (8 par + 2 mt + (p >> 1)) ^ fsw(row) = (8 par + 2 mt) ^ cx
+    const int q4 = (l & 15) >> 2, p4 = l & 3;
+    const int cx = (p4 >> 1) ^ fsw(8 * g + q4);
+    const int trb = F_OFF + 256 * (8 * g + q4) + 8 * (p4 & 1);
+    // X write lane bases: precision p at (4 (p ^ (g & 1)) + (q ^ phi)) units
+    const int xq = (b16 >> 2) ^ (3 * (wave >> 1));
+    const int xw0 = 128 * 4 * g + 16 * (4 * (g & 1) + xq) + 4 * (b16 & 3);
+    const int xw1 = 128 * 4 * g + 16 * (4 * ((g & 1) ^ 1) + xq) + 4 * (b16 & 3);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      // x of blocks 16h + b16: t = 32 ks + 8 g + j and t + 64 (j < 8)
+      float xv8[2][2][8];
+      const char* rowp = slot + XOFF + (16 * h + b16) * (B * ES);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt) {
+          if constexpr (ES == 4) {
+            const int u = 8 * ks + 2 * g + 16 * pt;
+            const float4 v0 = *reinterpret_cast<const float4*>(rowp + 16 * (u ^ b16));
+            const float4 v1 = *reinterpret_cast<const float4*>(rowp + 16 * ((u + 1) ^ b16));
+            xv8[ks][pt][0] = v0.x; xv8[ks][pt][1] = v0.y; xv8[ks][pt][2] = v0.z; xv8[ks][pt][3] = v0.w;
+            xv8[ks][pt][4] = v1.x; xv8[ks][pt][5] = v1.y; xv8[ks][pt][6] = v1.z; xv8[ks][pt][7] = v1.w;
+          } else {
+            const int u = 4 * ks + g + 8 * pt;
+            const uint4 w = *reinterpret_cast<const uint4*>(rowp + 16 * (u ^ b16));
+            const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float2 f = unpack16<XT>(ww[e]);
+              xv8[ks][pt][2 * e] = f.x;
+              xv8[ks][pt][2 * e + 1] = f.y;
+            }
+          }
+        }
+      float mx = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(xv8[ks][pt][j]));
+      const int sx = stat_scale_exp(2.f * wave_max(mx));   // |a|, |d| <= 2 max|x|
+      if (l == 0) wsc[par * 8 + wave * 2 + h] = sx - 7;     // X = D 2^-(sx - 7): the table's 2^-7
+      const float S = __int_as_float((sx + 127) << 23);
+      f32x4 acc[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        uint32_t ah[4], al[4], dh[4], dl[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float a0 = (xv8[ks][0][2 * e] + xv8[ks][1][2 * e]) * S;
+          const float a1 = (xv8[ks][0][2 * e + 1] + xv8[ks][1][2 * e + 1]) * S;
+          const float d0 = (xv8[ks][0][2 * e] - xv8[ks][1][2 * e]) * S;
+          const float d1 = (xv8[ks][0][2 * e + 1] - xv8[ks][1][2 * e + 1]) * S;
+          split2(a0, a1, ah[e], al[e]);
+          split2(d0, d1, dh[e], dl[e]);
+        }
+        const f16x8 bah = frag(ah[0], ah[1], ah[2], ah[3]), bal = frag(al[0], al[1], al[2], al[3]);
+        const f16x8 bdh = frag(dh[0], dh[1], dh[2], dh[3]), bdl = frag(dl[0], dl[1], dl[2], dl[3]);
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) {
+            // A = F^T (16 bins-reals x 32 t): two transposed reads of 4 rows each
+            const int cb = 16 * ((8 * pr + 2 * mt) ^ cx);
+            const char* p0 = lds + trb + 256 * 32 * ks + cb;
+            const s16x4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p0));
+            const s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p0 + 256 * 4));
+            const f16x8 af = __builtin_bit_cast(f16x8, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+            acc[4 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, pr ? bdh : bah, acc[4 * pr + mt], 0, 0, 0);
+            acc[4 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, pr ? bdl : bal, acc[4 * pr + mt], 0, 0, 0);
+          }
+      }
+      // D^T tile (pr, mt): rows 4g + r = cols of bins fA = 16 mt + 4 g + pr (r = 0, 1: re, im)
+      // and fA + 2 (r = 2, 3); column = input block 16 h + b16. Split and write 4 B per unit.
+      char* xb = slot + 8192 * h;
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          uint32_t hA, lA, hB, lB;
+          split2(acc[4 * pr + mt][0], acc[4 * pr + mt][1], hA, lA);
+          split2(acc[4 * pr + mt][2], acc[4 * pr + mt][3], hB, lB);
+          const int fo = 128 * (16 * mt + pr);
+          *reinterpret_cast<uint32_t*>(xb + xw0 + fo) = hA;
+          *reinterpret_cast<uint32_t*>(xb + xw1 + fo) = lA;
+          *reinterpret_cast<uint32_t*>(xb + xw0 + fo + 256) = hB;
+          *reinterpret_cast<uint32_t*>(xb + xw1 + fo + 256) = lB;
+        }
+    }
+  };
+
+  // ---- stage 2 (all waves): per-bin complex MAC on bins f = 8 wave + fb; Y units over the
+  // wave's own K-step-0 X units (the wave's DS operations execute in order)
+  auto stage2 = [&](char* region, int par) {
+    const int ml = opaque(lane);
+    const int arow = ml & 15, kb = ml >> 4;
+    const int a_t = arow >> 2, a_reim = (arow >> 1) & 1, a_prec = arow & 1;
+    const uint32_t a_sel = a_reim ? 0x01000302u : 0x03020100u;
+    const int yt = ml >> 4;
+    const int* sc = wsc + par * 8;
+    int nk[KS];
+    nk[0] = sc[a_t * 2];
+    nk[1] = sc[a_t * 2 + 1];
+    const int nmin = min(nk[0], nk[1]);
+    uint32_t amul[KS], amul0[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int d = nk[ks] - nmin;                  // factor 2^-d (fp16; subnormal / 0 far down)
+      const uint32_t hh = d <= 14 ? (uint32_t)(15 - d) << 10 : (d <= 24 ? 1u << (24 - d) : 0u);
+      const int d0 = d + 1;                          // bin 0: the inverse's 1/b vs 2/b
+      const uint32_t h0 = d0 <= 14 ? (uint32_t)(15 - d0) << 10 : (d0 <= 24 ? 1u << (24 - d0) : 0u);
+      amul[ks] = a_reim ? (hh | ((hh | 0x8000u) << 16)) : (hh | (hh << 16));
+      amul0[ks] = a_reim ? (h0 << 16) : h0;
+    }
+    const int xq = kb ^ (3 * (a_t >> 1));
+    const char* ab0 = region + a_t * SLOT + wave * 1024 + 16 * (4 * a_prec + xq);        // bins fb < 4
+    const char* ab1 = region + a_t * SLOT + wave * 1024 + 16 * (4 * (a_prec ^ 1) + xq);  // fb >= 4
+    uint4 araw[BW][KS];
+#pragma unroll
+    for (int fb = 0; fb < BW; ++fb)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        araw[fb][ks] = *reinterpret_cast<const uint4*>((fb < 4 ? ab0 : ab1) + 128 * fb + 8192 * ks);
+    uint32_t yh[BW][NT];
+#pragma unroll
+    for (int fb = 0; fb < BW; ++fb) {
+      const int f = wave * BW + fb;
+      f32x4 acc[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        uint4 raw = araw[fb][ks];
+        if (f == 0) {
+          raw.x = pkmul(raw.x, amul0[ks]); raw.y = pkmul(raw.y, amul0[ks]);
+          raw.z = pkmul(raw.z, amul0[ks]); raw.w = pkmul(raw.w, amul0[ks]);
+        } else {
+          raw.x = pkmul(__builtin_amdgcn_perm(raw.x, raw.x, a_sel), amul[ks]);
+          raw.y = pkmul(__builtin_amdgcn_perm(raw.y, raw.y, a_sel), amul[ks]);
+          raw.z = pkmul(__builtin_amdgcn_perm(raw.z, raw.z, a_sel), amul[ks]);
+          raw.w = pkmul(__builtin_amdgcn_perm(raw.w, raw.w, a_sel), amul[ks]);
+        }
+        const f16x8 a = __builtin_bit_cast(f16x8, raw);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, creg[fb][ks][nt], acc[nt], 0, 0, 0);
+      }
+      constexpr float YS = 1.f / 2097152.f;          // 2^-21: |Y| < 2^14 in fp16
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)                // rows 4 yt + {re hi, re lo, im hi, im lo}
+        yh[fb][nt] = pk_rne((acc[nt][0] + acc[nt][1]) * YS, (acc[nt][2] + acc[nt][3]) * YS);
+    }
+    char* yb = region + yt * SLOT + wave * 1024 + 16 * (ml & 15);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      *reinterpret_cast<uint4*>(yb + 16 * 16 * nt) = make_uint4(yh[0][nt], yh[2][nt], yh[4][nt], yh[6][nt]);
+      *reinterpret_cast<uint4*>(yb + 16 * (32 + 16 * nt)) = make_uint4(yh[1][nt], yh[3][nt], yh[5][nt], yh[7][nt]);
+    }
+  };
+
+  // ---- stage 3 (I wave, token slot j = wave - 4 of the previous tile): Y -> y, then the x DMA
+  // of tile mn into the freed slot. Returns the VMEM stores it issued after that DMA.
+  auto stage3 = [&](char* region, int par, int64_t mp, int64_t mn) {
+    const int l = opaque(lane);
+    const int o16 = l & 15, g = l >> 4;
+    char* slot = region + tslot * SLOT;
+    const int* sc = wsc + par * 8 + tslot * 2;
+    const int nmin = min(sc[0], sc[1]);
+    const float ysc = __builtin_ldexpf(inv_sc, 30 - nmin);
+    // all Y fragments of the token: B[k = 8 g + j][o] = unit(wave 4 ks + g, o, parity)
+    uint4 yf[KS][2][NT];
+    const char* yb = slot + g * 1024 + 16 * o16;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          yf[ks][pr][nt] = *reinterpret_cast<const uint4*>(yb + 4096 * ks + 16 * (32 * pr + 16 * nt));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot is free once read
+    if (mn < n_mtiles) dma_token(mn, region);
+    const int64_t tok = mp * TT + tslot;
+    const bool tok_ok = tok < n_tokens;
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (char*)yv + (tok_ok ? tok : 0) * M * ESY, 0, tok_ok ? (int)(M * ESY) : 0, 0x00020000);
+    const int nvalid = n_out - grp_o * NOG;
+    // table row reads: row 16 mt + o16, chunk (8 par + 4 ks + g) ^ fsw(o16)
+    const int gx = g ^ fsw(o16);
+    const char* gb = lds + F_OFF + 256 * o16;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      f16x8 gf[KS][2];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr)
+          gf[ks][pr] = *reinterpret_cast<const f16x8*>(gb + 4096 * mt + 16 * ((8 * pr + 4 * ks) ^ gx));
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        f32x4 E = f32x4{0.f, 0.f, 0.f, 0.f}, O = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          E = __builtin_amdgcn_mfma_f32_16x16x32_f16(gf[ks][0], __builtin_bit_cast(f16x8, yf[ks][0][nt]), E, 0, 0, 0);
+          O = __builtin_amdgcn_mfma_f32_16x16x32_f16(gf[ks][1], __builtin_bit_cast(f16x8, yf[ks][1][nt]), O, 0, 0, 0);
+        }
+        // rows t = 16 mt + 4 g + r, column o = 16 nt + o16
+        const int o = 16 * nt + o16;
+        const int64_t col = (int64_t)(grp_o * NOG + o) * B + 16 * mt + 4 * g;
+        const bool ovalid = o < nvalid;
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float os = O[r] * ysc;
+            v[r] = hf ? fmaf(E[r], ysc, -os) : fmaf(E[r], ysc, os);
+          }
+          const int64_t cc = col + 64 * hf;
+          if (Y32 || bias_dt != BCFFT_NONE) {       // .to(x dtype) :266, + bias :270-271
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = round_to(v[r], XT);
+            if (bias_dt != BCFFT_NONE && ovalid) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] += load_scalar(bias, cc + r, bias_dt);
+            }
+          }
+          const int yoff = ovalid ? (int)(cc * ESY) : 0x7fff0000;
+          if constexpr (Y32) {
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(u32x4, make_float4(v[0], v[1], v[2], v[3])), yrs, yoff, 0, 0);
+          } else {
+            const u32x2 pk = {pack16<XT>(v[0], v[1]), pack16<XT>(v[2], v[3])};
+            __builtin_amdgcn_raw_buffer_store_b64(pk, yrs, yoff, 0, 0);
+          }
+        }
+      }
+    }
+  };
+
+  // Pipeline, two workgroup barriers per M-tile. Iteration it (region R = it & 1 holds tile m,
+  // the other R' tile m - gstride):
+  //   P1  F waves: stage 1 of tile m in R.  I waves: stage 3 of tile m - gstride from R' (its
+  //       Y read first, then the LDS-DMA of x(m + gstride) into the freed slot of R', then
+  //       the y stores)                                                            | Ba |
+  //   P2  all waves: stage 2 of tile m in R; I waves then wait for their DMA       | Bb |
+  int64_t m = wg_in_grp;
+  for (int it = 0; m < n_mtiles || it > 0; ++it, m += gstride) {
+    char* region = lds + (it & 1) * REGION;
+    char* other = lds + ((it + 1) & 1) * REGION;
+    const int par = it & 1;
+    const bool have_f = m < n_mtiles;
+    if (fwave) {
+      if (have_f) stage1(region, par);
+    } else if (it > 0) {
+      stage3(other, par ^ 1, m - gstride, m + gstride);
+    } else if (m + gstride < n_mtiles) {
+      dma_token(m + gstride, other);
+    }
+    if (!have_f) break;
+    lds_barrier();                                  // Ba: X units and scales complete
+    stage2(region, par);
+    if (!fwave) wait_vmcnt<0>();                    // the next tile's x has landed (and the stores)
+    lds_barrier();                                  // Bb: Y units complete, x(m + gstride) staged
+  }
+}
+
+}  // namespace bcfft
+
+namespace {
+template <int XT, bool YF32>
+void launch_dm(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt, void* y,
+               hipStream_t s) {
+  const int groups = (n_out + 31) / 32;
+  const bcfft::SpecLayout sl = bcfft::spec_layout(n_out, 32, 128);
+  const int64_t n_mtiles = (n + 3) / 4;
+  int64_t total = bcfft::device_cu_count();
+  if (total > groups * n_mtiles) total = groups * n_mtiles;
+  if (total < groups) total = groups;
+  const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
+  hipLaunchKernelGGL((bcfft::bc_forward_dm_kernel<XT, YF32>), dim3((unsigned)total), dim3(512), 0, s, x, n,
+                     n_out, stat, bias, bias_dt, y);
+}
+}  // namespace
+
+namespace bcfft {
+bool dm_eligible(int n_in, int b) { return b == 128 && n_in == 32; }
+
+bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, const void* x, int64_t n, int n_out,
+                       const void* spec, const void* bias, int bias_dt, void* y, hipStream_t s) {
+  if (!dm_eligible(n_in, b)) return false;
+  if (xdt == BCFFT_F32) launch_dm<BCFFT_F32, true>(x, n, n_out, spec, bias, bias_dt, y, s);
+  else if (xdt == BCFFT_F16 && yf32) launch_dm<BCFFT_F16, true>(x, n, n_out, spec, bias, bias_dt, y, s);
+  else if (xdt == BCFFT_F16) launch_dm<BCFFT_F16, false>(x, n, n_out, spec, bias, bias_dt, y, s);
+  else if (yf32) launch_dm<BCFFT_BF16, true>(x, n, n_out, spec, bias, bias_dt, y, s);
+  else launch_dm<BCFFT_BF16, false>(x, n, n_out, spec, bias, bias_dt, y, s);
+  return true;
+}
+}  // namespace bcfft

@@ -73,14 +73,6 @@ struct GeoS {
 template <int L>
 __device__ __forceinline__ int k1_of(int j) { return L == 4 ? ((j == 1) ? 2 : (j == 2) ? 1 : j) : j; }
 
-template <int CTRL>
-__device__ __forceinline__ float dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
-}
-constexpr int DPP_XOR1 = 0xB1;   // quad_perm [1,0,3,2]
-constexpr int DPP_XOR2 = 0x4E;   // quad_perm [2,3,0,1]
-constexpr int DPP_XOR3 = 0x1B;   // quad_perm [3,2,1,0]
-constexpr int DPP_P0 = 0xB4;     // quad_perm [0,1,3,2]
 
 // L-point DFT across the L lanes of a transform, for each of the 16 registers (four-step
 // step 3). Radix-2 DPP stages with lane-constant coefficients; lane j ends with bins
@@ -304,14 +296,6 @@ __host__ __device__ inline void stat_decode(int j, double d[4]) {
   }
 }
 
-// v_mov through inline asm: the compiler cannot hoist or CSE what depends on it, so per-lane
-// addresses are rematerialised inside each phase instead of being kept (and spilled) across the
-// persistent loop next to the 128 VGPRs of stationary weights
-__device__ __forceinline__ int opaque(int v) {
-  int r;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
-  return r;
-}
 
 // the forward storage of stat_decode<L, false> as a complex factor: true = sigma_j * stored
 template <int L>
@@ -327,27 +311,6 @@ __host__ __device__ inline void stat_sigma(int j, double sg[2]) {
 #define MARK(n) do {} while (0)
 #endif
 
-// packed fp16 product of two fp16 pairs (v_pk_mul_f16)
-__device__ __forceinline__ uint32_t pkmul(uint32_t a, uint32_t b) {
-  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2, a) * __builtin_bit_cast(f16x2, b));
-}
-
-// max over the wave's 64 lanes, uniform: quad and row by DPP, the four rows by readlane
-__device__ __forceinline__ float wave_max(float v) {
-  v = fmaxf(v, dpp<DPP_XOR1>(v));
-  v = fmaxf(v, dpp<DPP_XOR2>(v));
-  v = fmaxf(v, dpp<0x141>(v));                     // row_half_mirror
-  v = fmaxf(v, dpp<0x140>(v));                     // row_mirror
-  const int u = __float_as_int(v);
-  const float a = fmaxf(__int_as_float(__builtin_amdgcn_readlane(u, 0)), __int_as_float(__builtin_amdgcn_readlane(u, 16)));
-  const float b = fmaxf(__int_as_float(__builtin_amdgcn_readlane(u, 32)), __int_as_float(__builtin_amdgcn_readlane(u, 48)));
-  return fmaxf(a, b);
-}
-// scale exponent for fp16 hi/lo: 2^nsc mx < 2^15, clamped so 2^nsc and 2^-nsc stay normal
-__device__ __forceinline__ int stat_scale_exp(float mx) {
-  const int nsc = 15 - __builtin_amdgcn_frexp_expf(mx);
-  return nsc < -126 ? -126 : (nsc > 126 ? 126 : nsc);
-}
 
 // x staging swizzle (16-B units of a row) that keeps the forward DPP-group reads conflict-free
 template <int L, int ES>

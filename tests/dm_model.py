@@ -1,0 +1,124 @@
+"""Numpy mirror of bc_forward_dm_kernel's dataflow (llama-fft_amd/csrc/bcfft_dm.hip) — test
+infrastructure.
+
+It restates, in the kernel's index conventions and roundings, the three matrix-core stages, so
+the decomposition, the DFT table (csrc/bcfft_dm_table.h, parsed here) and the scale bookkeeping
+are checked on the CPU against the oracle before the GPU runs them:
+
+  stage 1  per (token, half h of 16 input blocks): s = 2^sx with 2^sx * 2 max|x| < 2^15;
+           a_t = (x_t + x_{t+64}) s, d_t = (x_t - x_{t+64}) s (t < 64), each split into fp16
+           hi (round toward zero) + lo; X = [a Fe | d Fo] with the fp16 table F = DFT * 2^-7
+           (fp32 accumulation), i.e. X * 2^(sx - 7); split again into fp16 hi + lo.
+  stage 2  per packed bin: the halves brought to the token's smaller exponent (exact), times the
+           STAT image conj(C)/(2b) s_C (fp16), bin 0 with an extra 1/2; Y16 = fp16(Y * 2^-21).
+  stage 3  E = Fe Y16_even, O = Fo Y16_odd (fp32 accumulation); y_t = (E + O) sc,
+           y_{t+64} = (E - O) sc with sc = 2^(30 - nmin) / s_C.
+"""
+import os
+import re
+
+import numpy as np
+
+_TABLE = os.path.join(os.path.dirname(__file__), "..", "llama-fft_amd", "csrc", "bcfft_dm_table.h")
+
+
+def dm_table():
+    """F[t][col] * 2^-7 (64 x 128) exactly as the kernel's fp16 table holds it."""
+    words = [int(w, 16) for w in re.findall(r"0x([0-9a-f]{8})u", open(_TABLE).read())]
+    w = np.array(words, dtype=np.uint32).reshape(64, 64)
+    bits = np.empty((64, 128), dtype=np.uint16)
+    bits[:, 0::2] = (w & 0xFFFF).astype(np.uint16)
+    bits[:, 1::2] = (w >> 16).astype(np.uint16)
+    return bits.view(np.float16).astype(np.float64)
+
+
+def _rtz16(v):
+    """fp32 -> fp16 round toward zero (v_cvt_pkrtz_f16_f32), as float64."""
+    v = np.asarray(v, dtype=np.float32).astype(np.float64)
+    r = v.astype(np.float16).astype(np.float64)            # nearest
+    over = np.abs(r) > np.abs(v)
+    nxt = np.nextafter(r.astype(np.float16), np.float16(0)).astype(np.float64)
+    return np.where(over, nxt, r)
+
+
+def _split16(v):
+    hi = _rtz16(v)
+    lo = _rtz16(np.asarray(v, np.float32).astype(np.float64) - hi)
+    return hi, lo
+
+
+def _scale_exp(mx):
+    """stat_scale_exp: 15 - frexp exponent, clamped to [-126, 126]."""
+    e = np.frexp(np.float32(mx))[1]
+    return int(np.clip(15 - e, -126, 126))
+
+
+def stat_image(c):
+    """conj(C)/(2b) s_C as fp16 values (the STAT image's arithmetic), packed bins, and 1/s_C."""
+    b = c.shape[-1]
+    h = b // 2
+    xf = np.fft.rfft(c.astype(np.float64), axis=-1) / (2.0 * b)
+    p = xf[..., :h].astype(np.complex64).astype(np.complex128)
+    p[..., 0] = np.float32(xf[..., 0].real) + 1j * np.float32(xf[..., h].real)
+    mx = max(np.abs(p.real).max(), np.abs(p.imag).max())
+    n2 = int(np.clip(15 - np.frexp(np.float32(mx))[1], -126, 127))
+    sc = 2.0 ** n2
+    re = (p.real * sc).astype(np.float32).astype(np.float16).astype(np.float64)
+    im = (p.imag * sc).astype(np.float32).astype(np.float16).astype(np.float64)
+    return re, im, 1.0 / sc                                  # im of bins > 0 are Im(C) (not conj)
+
+
+def dm_forward(x, c):
+    """x (N, K) float32, c (nO, nI, 128): the kernel's fp32 output (no bias)."""
+    n, k = x.shape
+    no, ni, b = c.shape
+    assert b == 128 and ni * b == k and ni % 16 == 0
+    h = 64
+    F = dm_table()
+    Fe, Fo = F[:, :64], F[:, 64:]
+    cre, cim, inv_sc = stat_image(c)
+    y = np.zeros((n, no * b))
+    halves = ni // 16
+    for tok in range(n):
+        xr = x[tok].astype(np.float32).reshape(ni, b).astype(np.float64)
+        X = np.zeros((ni, h), dtype=np.complex128)
+        nsc = []
+        for hh in range(halves):
+            blk = xr[16 * hh:16 * hh + 16]
+            sx = _scale_exp(2.0 * np.abs(blk).max())
+            s = 2.0 ** sx
+            lo, hi = blk[:, :64], blk[:, 64:]
+            a = ((lo + hi).astype(np.float32) * np.float32(s)).astype(np.float64)
+            d = ((lo - hi).astype(np.float32) * np.float32(s)).astype(np.float64)
+            ah, al = _split16(a)
+            dh, dl = _split16(d)
+            ev = (ah @ Fe + al @ Fe).astype(np.float32)          # (16, 64): even packed bins
+            od = (dh @ Fo + dl @ Fo).astype(np.float32)
+            # packed bins: even f = 2j at ev[:, 2j], ev[:, 2j+1]; odd f = 2j+1 at od[:, 2j], od[:, 2j+1]
+            pk = np.zeros((16, 64, 2))
+            pk[:, 0::2, 0], pk[:, 0::2, 1] = ev[:, 0::2], ev[:, 1::2]
+            pk[:, 1::2, 0], pk[:, 1::2, 1] = od[:, 0::2], od[:, 1::2]
+            shi, slo = _split16(pk)
+            X[16 * hh:16 * hh + 16] = (shi[..., 0] + slo[..., 0]) + 1j * (shi[..., 1] + slo[..., 1])
+            nsc.append(sx - 7)
+        nmin = min(nsc)
+        for hh in range(halves):                                  # exact power-of-two alignment
+            X[16 * hh:16 * hh + 16] *= 2.0 ** (nmin - nsc[hh])
+        # stage 2: complex MAC per bin, bin 0 as two real products with the extra 1/2
+        yr = np.einsum("oif,if->of", cre[..., 1:], X.real[:, 1:]) - np.einsum("oif,if->of", cim[..., 1:], X.imag[:, 1:])
+        yi = np.einsum("oif,if->of", cre[..., 1:], X.imag[:, 1:]) + np.einsum("oif,if->of", cim[..., 1:], X.real[:, 1:])
+        y0 = 0.5 * np.einsum("oi,i->o", cre[..., 0], X.real[:, 0])
+        y64 = 0.5 * np.einsum("oi,i->o", cim[..., 0], X.imag[:, 0])
+        Y = np.zeros((no, 64, 2))
+        Y[:, 1:, 0], Y[:, 1:, 1] = yr, yi
+        Y[:, 0, 0], Y[:, 0, 1] = y0, y64
+        Y16 = (Y.astype(np.float32) * np.float32(2.0 ** -21)).astype(np.float16).astype(np.float64)
+        # stage 3: columns in table order
+        ye = np.stack([Y16[:, 0::2, 0], Y16[:, 0::2, 1]], -1).reshape(no, 64)
+        yo = np.stack([Y16[:, 1::2, 0], Y16[:, 1::2, 1]], -1).reshape(no, 64)
+        E = (ye @ Fe.T).astype(np.float32).astype(np.float64)   # (no, 64 t)
+        O = (yo @ Fo.T).astype(np.float32).astype(np.float64)
+        sc = 2.0 ** (30 - nmin) * inv_sc
+        yt = np.concatenate([(E + O) * sc, (E - O) * sc], -1)
+        y[tok] = yt.reshape(-1)
+    return y.astype(np.float32)

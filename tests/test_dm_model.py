@@ -1,0 +1,33 @@
+"""CPU checks of the DFT-on-MFMA kernel's decomposition (tests/dm_model.py) against the oracle:
+the table, the even/odd split, the packed-bin order, the scale bookkeeping and the fp16
+roundings reproduce the reference forward (patch_llama_fft.py:226-275) within the kernel's
+parity tolerance, before any GPU run."""
+import numpy as np
+import pytest
+
+from dm_model import dm_forward, dm_table
+from oracle import bc_oracle as orc
+
+
+def test_table_matches_dft():
+    F = dm_table() * 2.0 ** 7
+    t = np.arange(64)
+    assert np.allclose(F[:, 0], 1) and np.allclose(F[:, 1], (-1.0) ** t)
+    assert np.allclose(F[:, 2 * 5], np.cos(2 * np.pi * 5 * t / 64), atol=1e-3)
+    assert np.allclose(F[:, 64 + 2 * 5 + 1], -np.sin(2 * np.pi * 11 * t / 128), atol=1e-3)
+
+
+@pytest.mark.parametrize("scale", [1.0, 1e-5, 3e4])
+def test_dm_model_vs_oracle(scale):
+    rng = np.random.default_rng(7)
+    x = (rng.standard_normal((6, 4096)) * scale).astype(np.float32)
+    x[1] *= 1e3                                    # token scales differ
+    x[2, 100] = 500 * scale                        # one big channel in half 0
+    c = (rng.standard_normal((32, 32, 128)) * 0.01).astype(np.float32)
+    ref = orc.bc_forward(x, c)
+    got = dm_forward(x, c)
+    rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
+    assert rel < 4e-4, rel
+    for t in range(x.shape[0]):                   # per token as well
+        r = np.linalg.norm(got[t] - ref[t]) / np.linalg.norm(ref[t])
+        assert r < 6e-4, (t, r)

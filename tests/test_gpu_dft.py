@@ -1,0 +1,121 @@
+"""GPU parity of the DFT-on-MFMA kernel (algo="dft", bcfft_dm.hip) against the CPU oracle and
+against its numpy mirror (tests/dm_model.py).
+
+Numerics (dm_model.py): the table, C and Y are one fp16 term each, a/d and X two; fp32
+accumulation. Measured on the model: ~3.5e-4 relative Frobenius on random data. The tests assert
+< 6e-4 (north star: 1e-3), per token where scales differ; 16-bit outputs within ~1 output ulp
+plus the norm bound."""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import rel_err
+from oracle import bc_oracle as O
+from test_gpu_stationary import TDT, ODT, _check, _run
+
+pytestmark = pytest.mark.gpu
+DFT_TOL = 6e-4
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    import bcfft
+    bcfft.load()
+    return torch.device("cuda:0")
+
+
+CASES = [
+    # (M, N, x dtype, module dtype, bias)
+    (4096, 1, "float32", "float32", True),        # one token: partial M-tile, 3 zero-filled slots
+    (4096, 4, "float32", "float32", False),
+    (4096, 37, "float32", "float32", True),
+    (4096, 301, "bfloat16", "bfloat16", False),   # ragged, many tiles per workgroup
+    (4096, 64, "float16", "float16", True),
+    (4096, 50, "bfloat16", "float32", True),      # promotion -> fp32 output
+    (11008, 31, "bfloat16", "bfloat16", False),   # 3 output groups, the last one partial
+    (11008, 9, "float32", "float32", True),
+    (1024, 23, "float32", "float32", False),      # a single partial group (32 of 8 blocks)
+    (4096, 2000, "float32", "float32", False),    # > 1 tile per workgroup on every CU
+]
+
+
+@pytest.mark.parametrize("m,n,xdt,mdt,bias", CASES)
+def test_dft_vs_oracle(dev, m, n, xdt, mdt, bias):
+    k, b = 4096, 128
+    rng = np.random.default_rng(m + n + len(xdt))
+    c = (rng.standard_normal((m // b, k // b, b)) * 0.01).astype(np.float32)
+    bv = (rng.standard_normal(m) * 0.1).astype(np.float32) if bias else None
+    x = rng.standard_normal((n, k)).astype(np.float32)
+    if n > 600:                                    # oracle on a slice, all tokens computed
+        y, _ = _run(dev, x, c, bv, xdt, mdt, algo="dft")
+        sl = slice(n - 300, n)
+        ref = O.bc_forward(x[sl], c, bv)
+        e = rel_err(y[sl].float().cpu().numpy(), ref)
+        assert e < DFT_TOL, e
+        return
+    y, ref = _run(dev, x, c, bv, xdt, mdt, algo="dft")
+    _check(y, ref, xdt)              # fp32: < 6e-4 (= DFT_TOL); 16-bit x: ~1 ulp of the rounding
+
+
+def test_dft_matches_numpy_model(dev):
+    """The kernel and its numpy mirror agree far below the quantisation error: same table,
+    splits, scales and packed-bin order (only the fp32 summation order differs)."""
+    from dm_model import dm_forward
+    rng = np.random.default_rng(11)
+    c = (rng.standard_normal((32, 32, 128)) * 0.01).astype(np.float32)
+    x = rng.standard_normal((8, 4096)).astype(np.float32)
+    x[1] *= 300.0
+    y, ref = _run(dev, x, c, None, "float32", "float32", algo="dft")
+    g = y.cpu().numpy()
+    mdl = dm_forward(x, c)
+    assert rel_err(g, mdl) < 2e-5, rel_err(g, mdl)
+    assert rel_err(g, ref) < DFT_TOL
+
+
+def test_dft_per_token_scale(dev):
+    """Tokens 10^9 apart in magnitude, zero tokens, one massive channel, a token far below fp16's
+    range: the per-(token, half) power-of-two scales keep every token at full relative accuracy."""
+    rng = np.random.default_rng(2)
+    c = (rng.standard_normal((32, 32, 128)) * 0.01).astype(np.float32)
+    x = rng.standard_normal((9, 4096)).astype(np.float32)
+    x[0] *= 1e4
+    x[1] *= 1e-5
+    x[2] = 0.0
+    x[3, 77] = 3000.0
+    x[4, 2100:2300] *= 1e3                # the two K halves at very different scales
+    x[5] *= 1e-30
+    y, ref = _run(dev, x, c, None, "float32", "float32", algo="dft")
+    g = y.cpu().numpy()
+    assert np.all(g[2] == 0.0)
+    for t in (0, 1, 3, 4, 5, 6, 7, 8):
+        e = rel_err(g[t], ref[t])
+        assert e < DFT_TOL, (t, e)
+
+
+def test_dft_full_size_and_linearity(dev):
+    """North-star size (4096^2, b=128, N=8192, fp32): oracle parity on a 256-token slice plus
+    linearity over all 8192 tokens, and run-to-run bit equality."""
+    from bcfft import ops
+    rng = np.random.default_rng(0)
+    c = (rng.standard_normal((32, 32, 128)) * 0.01).astype(np.float32)
+    x = rng.standard_normal((8192, 4096)).astype(np.float32)
+    spec = ops.spectra(torch.from_numpy(c).to(dev))
+    xt = torch.from_numpy(x).to(dev)
+    y = ops.forward(xt, spec, None, 128, 4096, algo="dft")
+    sl = slice(4000, 4256)
+    e = rel_err(y[sl].cpu().numpy(), O.bc_forward(x[sl], c))
+    assert e < DFT_TOL, e
+    assert torch.equal(y, ops.forward(xt, spec, None, 128, 4096, algo="dft"))
+    x2 = torch.randn(8192, 4096, device=dev)
+    lhs = ops.forward(2.0 * xt + x2, spec, None, 128, 4096, algo="dft")
+    rhs = 2.0 * y + ops.forward(x2, spec, None, 128, 4096, algo="dft")
+    assert ((lhs - rhs).norm() / rhs.norm()).item() < 1e-3
+
+
+def test_dft_rejects_ineligible_geometry(dev):
+    from bcfft import ops
+    c = torch.zeros(4, 8, 64, device=dev)
+    spec = ops.spectra(c)
+    with pytest.raises(RuntimeError, match="block_size"):
+        ops.forward(torch.zeros(3, 512, device=dev), spec, None, 64, 256, algo="dft")
