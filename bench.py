@@ -50,6 +50,11 @@ def resolved_kernel(algo, k, b):
     mirrors bcfft_forward_algo's AUTO rule (csrc/bcfft_kernels.hip)."""
     n_in = k // b
     stat_ok = (b == 128 and n_in == 32) or (b == 64 and n_in in (32, 64))
+    dft_ok = b == 128 and n_in == 32
+    if algo == "dft" or (algo == "auto" and dft_ok):
+        return ("dft", "bc_forward_dm_kernel",
+                "MFMA fp16 throughout: block DFT (even/odd split, x hi+lo) x 2^-7 table, stationary "
+                "conj(C)*s_C MAC (X hi+lo), inverse DFT; f32 accumulate")
     if algo == "stationary" or (algo == "auto" and stat_ok):
         return ("stationary", "bc_forward_stat_kernel",
                 "MFMA fp16: conj(C)*s_C (VGPR-resident) x per-token-scaled X split hi+lo, f32 accumulate")
@@ -232,6 +237,8 @@ def main():
         # the north star in bf16 and on the other engines, and the config-4 sweep b x shape (bf16)
         vlist = [(4096, 4096, 64, "fp32", 128, "auto"),
                  (4096, 4096, 128, "bf16", 8192, "auto"),
+                 (4096, 4096, 128, "fp32", 8192, "stationary"),
+                 (4096, 4096, 128, "bf16", 8192, "stationary"),
                  (4096, 4096, 128, "fp32", 8192, "mfma"),
                  (4096, 4096, 128, "fp32", 8192, "valu")]
         for vb in (64, 128, 256):

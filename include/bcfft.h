@@ -46,7 +46,7 @@ enum bcfft_dtype { BCFFT_NONE = -1, BCFFT_F32 = 0, BCFFT_F16 = 1, BCFFT_BF16 = 2
  *  DFT:  the STAT weights, with the forward and inverse DFTs of the blocks also on the matrix
  *        cores (dense fp16 GEMMs against a 2^-7-scaled DFT table, even/odd split) instead of
  *        VALU FFTs; ~3.5e-4 relative. Geometry: block_size 128 with in_features 4096.
- *  AUTO: STAT where eligible, else MFMA for block_size <= 128, else VALU. */
+ *  AUTO: DFT where eligible, else STAT where eligible, else MFMA for block_size <= 128, else VALU. */
 enum bcfft_algo { BCFFT_ALGO_AUTO = 0, BCFFT_ALGO_MFMA = 1, BCFFT_ALGO_VALU = 2, BCFFT_ALGO_STAT = 3,
                   BCFFT_ALGO_DFT = 4 };
 

@@ -108,7 +108,8 @@ def default_algo() -> str:
 def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, block_size: int,
             out_features: int, algo: str | None = None) -> torch.Tensor:
     """y = BC(x2d) (+ bias) with one fused kernel. x2d: (N, K) device tensor.
-    algo: "auto" (stationary where eligible, else mfma for b <= 128, else valu),
+    algo: "auto" (dft where eligible, else stationary where eligible, else mfma for b <= 128,
+    else valu), "dft" (block DFTs and MAC on fp16 MFMA, weights in VGPRs, ~3.5e-4),
     "stationary" (weights in VGPRs, fp16 MFMA, ~3e-4), "mfma" (split-bf16, ~1e-5) or
     "valu" (exact fp32 MAC). See include/bcfft.h."""
     _lib.require_device(x2d, "bcfft.forward")

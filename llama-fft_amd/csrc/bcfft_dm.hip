@@ -18,15 +18,20 @@
 //    LDS-DMA; then all 8 waves run the per-bin complex MAC (stage 2) on their 8 bins, exactly as
 //    the stationary kernel. Two workgroup barriers per M-tile, two 64 KiB LDS regions.
 //  * Numerics: a, d split into fp16 hi + lo under a per-(token, 16-block half) power-of-two
-//    scale; X split into hi + lo; C and the table one fp16 term each; Y one fp16 term (a fixed
-//    2^-21 keeps it in range); fp32 accumulation everywhere: ~3.5e-4 relative on the layer
-//    output (tests/dm_model.py restates it; north star: 1e-3).
+//    scale; X split into hi + lo; Y split into hi + lo (a fixed 2^-21 keeps it in range;
+//    BCFFT_DM_YSPLIT=0 builds one RNE term: ~10 % faster, ~3.5e-4); C and the table one fp16
+//    term each; fp32 accumulation everywhere: ~2.8e-4 relative on the layer output, linear in x
+//    to ~1e-6 (tests/dm_model.py restates it; north star: 1e-3).
 //
 // Geometry: b = 128 with K = 4096 (32 input blocks: two K-steps of 16), any M (output groups of
 // 32 blocks), x fp32 / fp16 / bf16, y = promote(x, bias). LDS and register maps below; every
 // LDS access pattern is checked conflict-free by tools/lds_banks_dm.py.
 #include "bcfft_device.h"
 #include "bcfft_dm_table.h"
+
+#ifndef BCFFT_DM_YSPLIT
+#define BCFFT_DM_YSPLIT 1                   // Y as fp16 hi + lo (else one RNE term)
+#endif
 
 namespace bcfft {
 
@@ -72,7 +77,17 @@ __device__ __forceinline__ float hi16(uint32_t p) { return (float)__builtin_bit_
 // (a, b) -> fp16 hi (toward zero) and lo = the rest (toward zero)
 __device__ __forceinline__ void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
   hi = pk_rtz(a, b);
-  lo = pk_rtz(a - lo16(hi), b - hi16(hi));
+  lo = pk_rtz(__builtin_fmaf(a, 1.f, -lo16(hi)), __builtin_fmaf(b, 1.f, -hi16(hi)));   // v_fma_mix
+}
+// max |v| over the wave as an integer max of the magnitude bits (no NaN canonicalisation)
+__device__ __forceinline__ uint32_t wave_umax(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true));   // quad xor 1
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true));   // quad xor 2
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, true));  // row half mirror
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, true));  // row mirror
+  const uint32_t a = max((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16));
+  const uint32_t b = max((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48));
+  return max(a, b);
 }
 __device__ __forceinline__ f16x8 frag(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   return __builtin_bit_cast(f16x8, make_uint4(a, b, c, d));
@@ -88,9 +103,15 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
   constexpr bool Y32 = YF32 || XT == BCFFT_F32;
   constexpr int ESY = Y32 ? 4 : 2;
   constexpr int NPIECE = BW * KS * NT;
-  constexpr int XOFF = ES == 4 ? 0 : 8192;          // x rows within a token slot
   constexpr int NDMA = K * ES / 1024;               // 1-KiB LDS-DMA pieces per token
 
+  ANALYSIS_INIT;
+  bool sub_on = false;                              // sub-phase stamps (analysis builds: iteration 4)
+#ifdef BCFFT_MARKS
+#define SUBSTAMP(id) do { asm volatile(";MARK s" #id); if (sub_on) STAMP(id); } while (0)
+#else
+#define SUBSTAMP(id) do { if (sub_on) STAMP(id); } while (0)
+#endif
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
   int* wsc = reinterpret_cast<int*>(lds + SC_OFF);
 
@@ -109,13 +130,13 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
   // ---- x of one token -> its slot by LDS-DMA (I waves; the buffer range zero-fills tokens past
   // n_tokens). LDS is lane-linear per piece, so the slot's unit swizzle (logical 16-B unit u of
   // block row r at physical u ^ (r & 15)) is applied to the global source offsets.
-  auto dma_token = [&](int64_t m, char* region) {
+  auto dma_token = [&](int64_t m, char* region, int q0, int q1) {   // pieces [q0, q1)
     const int64_t tok = m * TT + tslot;
     const bool ok = tok < n_tokens;
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<char*>((const char*)xv) + (ok ? tok : 0) * K * ES, 0, ok ? K * ES : 0, 0x00020000);
     const int dl = opaque(lane);
-    const uint32_t dst0 = lds_base + (uint32_t)(region - lds) + tslot * SLOT + XOFF;
+    const uint32_t dst0 = lds_base + (uint32_t)(region - lds) + tslot * SLOT;
     if constexpr (ES == 4) {                        // piece q: rows 2q + (lane >> 5), 512 B each
       int vb[8];
 #pragma unroll
@@ -124,7 +145,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
         vb[c] = h * 512 + 16 * ((dl & 31) ^ ((2 * c + h) & 15));
       }
 #pragma unroll
-      for (int q = 0; q < NDMA; ++q) {
+      for (int q = q0; q < q1; ++q) {
         uint32_t keep;
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
                      : "=&s"(keep) : "v"(vb[q & 7]), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
@@ -137,7 +158,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
         vb[c] = r * 256 + 16 * ((dl & 15) ^ ((4 * c + r) & 15));
       }
 #pragma unroll
-      for (int q = 0; q < NDMA; ++q) {
+      for (int q = q0; q < q1; ++q) {
         uint32_t keep;
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
                      : "=&s"(keep) : "v"(vb[q & 3]), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
@@ -146,7 +167,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
   };
 
   // ---- prologue: first tile's x (I waves), the DFT table, the stationary B fragments
-  if (!fwave && wg_in_grp < n_mtiles) dma_token(wg_in_grp, lds);
+  if (!fwave && wg_in_grp < n_mtiles) dma_token(wg_in_grp, lds, 0, NDMA);
   {
     const uint4* tab = reinterpret_cast<const uint4*>(kDmF);
 #pragma unroll
@@ -186,10 +207,13 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     const int xw0 = 128 * 4 * g + 16 * (4 * (g & 1) + xq) + 4 * (b16 & 3);
     const int xw1 = 128 * 4 * g + 16 * (4 * ((g & 1) ^ 1) + xq) + 4 * (b16 & 3);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int hh = 0; hh < 2; ++hh) {
+      // 16-bit x sits in the slot's first 8 KiB: half 1 (bytes 4-8 KiB) goes first, so that the
+      // in-place X writes of half 1 (8-16 KiB) and then half 0 (0-8 KiB) clobber nothing unread
+      const int h = ES == 4 ? hh : 1 - hh;
       // x of blocks 16h + b16: t = 32 ks + 8 g + j and t + 64 (j < 8)
       float xv8[2][2][8];
-      const char* rowp = slot + XOFF + (16 * h + b16) * (B * ES);
+      const char* rowp = slot + (16 * h + b16) * (B * ES);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -212,16 +236,18 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
             }
           }
         }
-      float mx = 0.f;
+      SUBSTAMP(55 + 4 * hh);
+      uint32_t mx = 0u;                             // max |x| as magnitude bits
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int pt = 0; pt < 2; ++pt)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(xv8[ks][pt][j]));
-      const int sx = stat_scale_exp(2.f * wave_max(mx));   // |a|, |d| <= 2 max|x|
+          for (int j = 0; j < 8; ++j) mx = max(mx, __float_as_uint(xv8[ks][pt][j]) & 0x7fffffffu);
+      const int sx = stat_scale_exp(2.f * __uint_as_float(wave_umax(mx)));   // |a|, |d| <= 2 max|x|
       if (l == 0) wsc[par * 8 + wave * 2 + h] = sx - 7;     // X = D 2^-(sx - 7): the table's 2^-7
       const float S = __int_as_float((sx + 127) << 23);
+      SUBSTAMP(56 + 4 * hh);
       f32x4 acc[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -255,6 +281,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
       }
       // D^T tile (pr, mt): rows 4g + r = cols of bins fA = 16 mt + 4 g + pr (r = 0, 1: re, im)
       // and fA + 2 (r = 2, 3); column = input block 16 h + b16. Split and write 4 B per unit.
+      SUBSTAMP(57 + 4 * hh);
       char* xb = slot + 8192 * h;
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr)
@@ -269,6 +296,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
           *reinterpret_cast<uint32_t*>(xb + xw0 + fo + 256) = hB;
           *reinterpret_cast<uint32_t*>(xb + xw1 + fo + 256) = lB;
         }
+      SUBSTAMP(58 + 4 * hh);
     }
   };
 
@@ -304,7 +332,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
         araw[fb][ks] = *reinterpret_cast<const uint4*>((fb < 4 ? ab0 : ab1) + 128 * fb + 8192 * ks);
-    uint32_t yh[BW][NT];
+    constexpr bool YSP = BCFFT_DM_YSPLIT;
+    uint32_t yh[BW][NT], yl[BW][NT];
 #pragma unroll
     for (int fb = 0; fb < BW; ++fb) {
       const int f = wave * BW + fb;
@@ -331,18 +360,30 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
       constexpr float YS = 1.f / 2097152.f;          // 2^-21: |Y| < 2^14 in fp16
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)                // rows 4 yt + {re hi, re lo, im hi, im lo}
-        yh[fb][nt] = pk_rne((acc[nt][0] + acc[nt][1]) * YS, (acc[nt][2] + acc[nt][3]) * YS);
+      {
+        const float yr = (acc[nt][0] + acc[nt][1]) * YS, yi = (acc[nt][2] + acc[nt][3]) * YS;
+        if constexpr (YSP) split2(yr, yi, yh[fb][nt], yl[fb][nt]);
+        else yh[fb][nt] = pk_rne(yr, yi);
+      }
     }
     char* yb = region + yt * SLOT + wave * 1024 + 16 * (ml & 15);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       *reinterpret_cast<uint4*>(yb + 16 * 16 * nt) = make_uint4(yh[0][nt], yh[2][nt], yh[4][nt], yh[6][nt]);
       *reinterpret_cast<uint4*>(yb + 16 * (32 + 16 * nt)) = make_uint4(yh[1][nt], yh[3][nt], yh[5][nt], yh[7][nt]);
+      if constexpr (YSP) {                          // lo terms over the K-step-1 X units of these bins
+        *reinterpret_cast<uint4*>(yb + 8192 + 16 * 16 * nt) = make_uint4(yl[0][nt], yl[2][nt], yl[4][nt], yl[6][nt]);
+        *reinterpret_cast<uint4*>(yb + 8192 + 16 * (32 + 16 * nt)) = make_uint4(yl[1][nt], yl[3][nt], yl[5][nt], yl[7][nt]);
+      }
     }
   };
 
-  // ---- stage 3 (I wave, token slot j = wave - 4 of the previous tile): Y -> y, then the x DMA
-  // of tile mn into the freed slot. Returns the VMEM stores it issued after that DMA.
+  // ---- stage 3 (I wave, token slot j = wave - 4 of the previous tile): Y -> y rows staged in
+  // LDS and stored as 1 KiB contiguous buffer stores. The slot's Y units (first 8 KiB) are read
+  // into registers first; its K-step-1 X units (second 8 KiB) are dead after stage 2. 16-bit y:
+  // 32 rows x 256 B staged in the second 8 KiB, and the next tile's x (8 KiB) comes in by
+  // LDS-DMA over the first 8 KiB at once. fp32 y: N-tile 0's rows in the second 8 KiB, N-tile
+  // 1's in the first, and the next x (16 KiB) follows the read-back.
   auto stage3 = [&](char* region, int par, int64_t mp, int64_t mn) {
     const int l = opaque(lane);
     const int o16 = l & 15, g = l >> 4;
@@ -351,73 +392,137 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     const int nmin = min(sc[0], sc[1]);
     const float ysc = __builtin_ldexpf(inv_sc, 30 - nmin);
     // all Y fragments of the token: B[k = 8 g + j][o] = unit(wave 4 ks + g, o, parity)
-    uint4 yf[KS][2][NT];
+    constexpr bool YSP = BCFFT_DM_YSPLIT;
+    constexpr int NYP = YSP ? 2 : 1;                // Y precision terms (hi; lo 8 KiB further)
+    constexpr bool YSP_PREF_OFF = YSP;              // the lo terms take the table prefetch's VGPRs
+    uint4 yf[NYP][KS][2][NT];
     const char* yb = slot + g * 1024 + 16 * o16;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
+    for (int yp = 0; yp < NYP; ++yp)
 #pragma unroll
-      for (int pr = 0; pr < 2; ++pr)
+      for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-          yf[ks][pr][nt] = *reinterpret_cast<const uint4*>(yb + 4096 * ks + 16 * (32 * pr + 16 * nt));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot is free once read
-    if (mn < n_mtiles) dma_token(mn, region);
-    const int64_t tok = mp * TT + tslot;
-    const bool tok_ok = tok < n_tokens;
-    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
-        (char*)yv + (tok_ok ? tok : 0) * M * ESY, 0, tok_ok ? (int)(M * ESY) : 0, 0x00020000);
-    const int nvalid = n_out - grp_o * NOG;
+        for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            yf[yp][ks][pr][nt] = *reinterpret_cast<const uint4*>(yb + 8192 * yp + 4096 * ks + 16 * (32 * pr + 16 * nt));
     // table row reads: row 16 mt + o16, chunk (8 par + 4 ks + g) ^ fsw(o16)
     const int gx = g ^ fsw(o16);
     const char* gb = lds + F_OFF + 256 * o16;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      f16x8 gf[KS][2];
+    auto gload = [&](int mt, f16x8 (&gf)[KS][2]) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
         for (int pr = 0; pr < 2; ++pr)
           gf[ks][pr] = *reinterpret_cast<const f16x8*>(gb + 4096 * mt + 16 * ((8 * pr + 4 * ks) ^ gx));
+    };
+    f16x8 gcur[KS][2], gnxt[KS][2];
+    gload(0, gcur);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // Y is in registers: the slot is free
+    SUBSTAMP(55);
+    const bool dma = mn < n_mtiles;
+    if (ES == 2 && dma) dma_token(mn, region, 0, NDMA);
+    SUBSTAMP(56);
+    const int64_t tok = mp * TT + tslot;
+    const bool tok_ok = tok < n_tokens;
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (char*)yv + (tok_ok ? tok : 0) * M * ESY, 0, tok_ok ? (int)(M * ESY) : 0, 0x00020000);
+    const int nvalid = n_out - grp_o * NOG;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      if (!YSP_PREF_OFF && mt < 3) gload(mt + 1, gnxt);
+      f32x4 E[NT], O[NT];
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        f32x4 E = f32x4{0.f, 0.f, 0.f, 0.f}, O = f32x4{0.f, 0.f, 0.f, 0.f};
+        E[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        O[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          E = __builtin_amdgcn_mfma_f32_16x16x32_f16(gf[ks][0], __builtin_bit_cast(f16x8, yf[ks][0][nt]), E, 0, 0, 0);
-          O = __builtin_amdgcn_mfma_f32_16x16x32_f16(gf[ks][1], __builtin_bit_cast(f16x8, yf[ks][1][nt]), O, 0, 0, 0);
-        }
-        // rows t = 16 mt + 4 g + r, column o = 16 nt + o16
+      for (int yp = 0; yp < NYP; ++yp)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) {
+            E[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][0], __builtin_bit_cast(f16x8, yf[yp][ks][0][nt]), E[nt], 0, 0, 0);
+            O[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][1], __builtin_bit_cast(f16x8, yf[yp][ks][1][nt]), O[nt], 0, 0, 0);
+          }
+      // rows t = 16 mt + 4 g + r (and t + 64), column o = 16 nt + o16
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
         const int o = 16 * nt + o16;
-        const int64_t col = (int64_t)(grp_o * NOG + o) * B + 16 * mt + 4 * g;
-        const bool ovalid = o < nvalid;
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float os = O[r] * ysc;
-            v[r] = hf ? fmaf(E[r], ysc, -os) : fmaf(E[r], ysc, os);
+            const float os = O[nt][r] * ysc;
+            v[r] = hf ? fmaf(E[nt][r], ysc, -os) : fmaf(E[nt][r], ysc, os);
           }
-          const int64_t cc = col + 64 * hf;
           if (Y32 || bias_dt != BCFFT_NONE) {       // .to(x dtype) :266, + bias :270-271
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = round_to(v[r], XT);
-            if (bias_dt != BCFFT_NONE && ovalid) {
+            if (bias_dt != BCFFT_NONE && o < nvalid) {
+              const int64_t cc = (int64_t)(grp_o * NOG + o) * B + 16 * mt + 4 * g + 64 * hf;
 #pragma unroll
               for (int r = 0; r < 4; ++r) v[r] += load_scalar(bias, cc + r, bias_dt);
             }
           }
-          const int yoff = ovalid ? (int)(cc * ESY) : 0x7fff0000;
-          if constexpr (Y32) {
-            __builtin_amdgcn_raw_buffer_store_b128(
-                __builtin_bit_cast(u32x4, make_float4(v[0], v[1], v[2], v[3])), yrs, yoff, 0, 0);
-          } else {
-            const u32x2 pk = {pack16<XT>(v[0], v[1]), pack16<XT>(v[2], v[3])};
-            __builtin_amdgcn_raw_buffer_store_b64(pk, yrs, yoff, 0, 0);
+          if constexpr (Y32) {                      // N-tile nt's 16 rows, 16-B unit u of row o16
+            char* stg = slot + (nt ? 0 : 8192);
+            const int u = 4 * mt + g + 16 * hf;
+            *reinterpret_cast<float4*>(stg + 512 * o16 + 16 * (u ^ (o16 & 7))) = make_float4(v[0], v[1], v[2], v[3]);
+          } else {                                  // row o of the 32, 8-B unit v8
+            const int v8 = 4 * mt + g + 16 * hf;
+            const int sg = ((o & 7) << 1) | ((o >> 3) & 1);
+            *reinterpret_cast<uint2*>(slot + 8192 + 256 * o + 8 * (v8 ^ sg)) =
+                make_uint2(pack16<XT>(v[0], v[1]), pack16<XT>(v[2], v[3]));
           }
         }
       }
+      if (mt < 3) {
+        if (YSP_PREF_OFF) {
+          gload(mt + 1, gcur);                      // no prefetch: registers for the Y lo terms
+        } else {
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+            for (int pr = 0; pr < 2; ++pr) gcur[ks][pr] = gnxt[ks][pr];
+        }
+      }
     }
+    SUBSTAMP(57);
+    // staged rows -> global: each instruction stores 1 KiB = RPI whole y rows of the group
+    constexpr int RB = B * ESY, RPI = 1024 / RB, LPR = 64 / RPI;   // row bytes, rows/store, lanes/row
+    const int w = l & (LPR - 1);
+#pragma unroll
+    for (int half = 0; half < (Y32 ? 2 : 1); ++half) {   // 8 store instructions at a time
+      uint4 d[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int rr = 8 * RPI * half + q * RPI + (int)((unsigned)l / LPR);   // y row of the group
+        if constexpr (Y32) {
+          const int s16 = rr & 15;
+          const char* stg = slot + (rr >= 16 ? 0 : 8192);
+          d[q] = *reinterpret_cast<const uint4*>(stg + 512 * s16 + 16 * (w ^ (s16 & 7)));
+        } else {
+          uint4 v = *reinterpret_cast<const uint4*>(slot + 8192 + 256 * rr + 16 * (w ^ (rr & 7)));
+          if ((8 * RPI * half + q * RPI) & 8) v = make_uint4(v.z, v.w, v.x, v.y);   // 8-B halves swapped
+          d[q] = v;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int rr = 8 * RPI * half + q * RPI + (int)((unsigned)l / LPR);
+        const int yoff = rr < nvalid ? (grp_o * NOG + rr) * RB + 16 * w : 0x7fff0000;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs, yoff, 0, 0);
+      }
+    }
+    SUBSTAMP(58);
+    if constexpr (ES == 4) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // staged rows read back: slot free
+      if (dma) dma_token(mn, region, 0, NDMA);
+    }
+    SUBSTAMP(59);
   };
 
   // Pipeline, two workgroup barriers per M-tile. Iteration it (region R = it & 1 holds tile m,
@@ -427,24 +532,34 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
   //       the y stores)                                                            | Ba |
   //   P2  all waves: stage 2 of tile m in R; I waves then wait for their DMA       | Bb |
   int64_t m = wg_in_grp;
+  STAMP(0);
   for (int it = 0; m < n_mtiles || it > 0; ++it, m += gstride) {
     char* region = lds + (it & 1) * REGION;
     char* other = lds + ((it + 1) & 1) * REGION;
     const int par = it & 1;
     const bool have_f = m < n_mtiles;
+    const int sb = 1 + 6 * (it < 8 ? it : 8);       // stamp slots: iterations 0-7, then the latest
+    sub_on = it == 4;
+    STAMP(sb);
     if (fwave) {
       if (have_f) stage1(region, par);
     } else if (it > 0) {
       stage3(other, par ^ 1, m - gstride, m + gstride);
     } else if (m + gstride < n_mtiles) {
-      dma_token(m + gstride, other);
+      dma_token(m + gstride, other, 0, NDMA);
     }
+    STAMP(sb + 1);
     if (!have_f) break;
     lds_barrier();                                  // Ba: X units and scales complete
+    STAMP(sb + 2);
     stage2(region, par);
+    STAMP(sb + 3);
     if (!fwave) wait_vmcnt<0>();                    // the next tile's x has landed (and the stores)
+    STAMP(sb + 4);
     lds_barrier();                                  // Bb: Y units complete, x(m + gstride) staged
+    STAMP(sb + 5);
   }
+  STAMP(63);
 }
 
 }  // namespace bcfft
@@ -464,6 +579,18 @@ void launch_dm(const void* x, int64_t n, int n_out, const void* spec, const void
                      n_out, stat, bias, bias_dt, y);
 }
 }  // namespace
+
+#if defined(BCFFT_ABLATE) || defined(BCFFT_STAMPS)
+// analysis builds only: stamp buffer of bc_forward_dm_kernel (this TU's copy). Slots per wave:
+// 0 start | per M-tile it (base 1 + 6 min(it, 8)): +0 loop top, +1 stage 1 / stage 3 done,
+// +2 after Ba, +3 stage 2 done, +4 DMA landed (I waves), +5 after Bb | 55-62 sub-phases of
+// iteration 4 (F waves, per half: x read, scale, MFMAs, X written; I waves: Y read, DMA issued,
+// per N-tile computed + stored, DMA 2 issued) | 63 end
+extern "C" int bcfft_set_stamps_dm(void* buf) {
+  unsigned long long* p = (unsigned long long*)buf;
+  return hipMemcpyToSymbol(HIP_SYMBOL(bcfft::g_stamps), &p, sizeof(p)) == hipSuccess ? 0 : BCFFT_ERR_HIP;
+}
+#endif
 
 namespace bcfft {
 bool dm_eligible(int n_in, int b) { return b == 128 && n_in == 32; }

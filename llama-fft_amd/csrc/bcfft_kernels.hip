@@ -736,6 +736,7 @@ int bcfft_spectra(const void* c, int c_dtype, int n_out_blocks, int n_in_blocks,
 // the algorithm bcfft_forward_algo runs for this geometry (AUTO resolved)
 static int resolve_algo(int algo, int n_in, int block_size) {
   if (algo != BCFFT_ALGO_AUTO) return algo;
+  if (bcfft::dm_eligible(n_in, block_size)) return BCFFT_ALGO_DFT;
   return bcfft::stat_eligible(n_in, block_size) ? BCFFT_ALGO_STAT
                                                 : (block_size <= 128 ? BCFFT_ALGO_MFMA : BCFFT_ALGO_VALU);
 }

@@ -10,7 +10,8 @@ are checked on the CPU against the oracle before the GPU runs them:
            hi (round toward zero) + lo; X = [a Fe | d Fo] with the fp16 table F = DFT * 2^-7
            (fp32 accumulation), i.e. X * 2^(sx - 7); split again into fp16 hi + lo.
   stage 2  per packed bin: the halves brought to the token's smaller exponent (exact), times the
-           STAT image conj(C)/(2b) s_C (fp16), bin 0 with an extra 1/2; Y16 = fp16(Y * 2^-21).
+           STAT image conj(C)/(2b) s_C (fp16), bin 0 with an extra 1/2; Y * 2^-21 split into fp16
+           hi + lo (ysplit, the product build) or rounded once to fp16.
   stage 3  E = Fe Y16_even, O = Fo Y16_odd (fp32 accumulation); y_t = (E + O) sc,
            y_{t+64} = (E - O) sc with sc = 2^(30 - nmin) / s_C.
 """
@@ -68,7 +69,7 @@ def stat_image(c):
     return re, im, 1.0 / sc                                  # im of bins > 0 are Im(C) (not conj)
 
 
-def dm_forward(x, c):
+def dm_forward(x, c, ysplit=True):
     """x (N, K) float32, c (nO, nI, 128): the kernel's fp32 output (no bias)."""
     n, k = x.shape
     no, ni, b = c.shape
@@ -112,7 +113,12 @@ def dm_forward(x, c):
         Y = np.zeros((no, 64, 2))
         Y[:, 1:, 0], Y[:, 1:, 1] = yr, yi
         Y[:, 0, 0], Y[:, 0, 1] = y0, y64
-        Y16 = (Y.astype(np.float32) * np.float32(2.0 ** -21)).astype(np.float16).astype(np.float64)
+        ys = (Y.astype(np.float32) * np.float32(2.0 ** -21)).astype(np.float32)
+        if ysplit:
+            yh, yl = _split16(ys)
+            Y16 = yh + yl
+        else:
+            Y16 = ys.astype(np.float16).astype(np.float64)
         # stage 3: columns in table order
         ye = np.stack([Y16[:, 0::2, 0], Y16[:, 0::2, 1]], -1).reshape(no, 64)
         yo = np.stack([Y16[:, 1::2, 0], Y16[:, 1::2, 1]], -1).reshape(no, 64)

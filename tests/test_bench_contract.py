@@ -18,7 +18,8 @@ def test_algorithmic_bytes_match_survey():
 
 
 def test_engine_resolution_mirrors_auto_rule():
-    assert bench.resolved_kernel("auto", 4096, 128)[1] == "bc_forward_stat_kernel"
+    assert bench.resolved_kernel("auto", 4096, 128)[1] == "bc_forward_dm_kernel"
+    assert bench.resolved_kernel("stationary", 4096, 128)[1] == "bc_forward_stat_kernel"
     assert bench.resolved_kernel("auto", 4096, 64)[1] == "bc_forward_stat_kernel"
     assert bench.resolved_kernel("auto", 2048, 64)[1] == "bc_forward_stat_kernel"
     assert bench.resolved_kernel("auto", 11008, 128)[1] == "bc_forward_mfma_kernel"
@@ -42,4 +43,4 @@ def test_bench_prints_one_contract_line():
     r = d["roofline"]
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
-    assert r["kernel"] == "bc_forward_stat_kernel"
+    assert r["kernel"] == "bc_forward_dm_kernel"

@@ -134,7 +134,7 @@ def test_forward_workspace_bytes_without_gpu(built_lib):
     assert ws(1700, 11008, 4096, 128, AUTO) == 2 * 1700 * 4096 * 4     # prefill batch: 2 slices
     assert ws(2040, 11008, 4096, 128, AUTO) == 2 * 2040 * 4096 * 4     # 255 rows < 256 CUs
     assert ws(2048, 11008, 4096, 128, AUTO) == 0                    # 256 rows: full grid
-    assert ws(100, 4096, 4096, 128, AUTO) == 0                      # stationary
+    assert ws(100, 4096, 4096, 128, AUTO) == 0                      # DFT kernel (persistent)
     assert ws(100, 4096, 4096, 128, MFMA) == 2 * 100 * 4096 * 4        # forced MFMA: 4 chunks
     assert ws(100, 3072, 4096, 128, MFMA) == 0                      # 3 chunks: never split
     assert ws(50, 11008, 4096, 128, VALU) == 22 * 50 * 4096 * 4     # VALU b = 128: 22 chunks of 4 blocks

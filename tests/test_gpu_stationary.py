@@ -88,13 +88,18 @@ def test_stationary_vs_oracle(dev, k, m, b, n, xdt, mdt, bias):
     _check(y, ref, xdt)
 
 
-def test_stationary_is_auto_for_eligible_shapes(dev):
-    """AUTO picks the stationary kernel at 4096^2 b=128: same bits as algo=stationary."""
+def test_auto_resolution_for_eligible_shapes(dev):
+    """AUTO picks the DFT-on-MFMA kernel at 4096^2 b=128 and the stationary kernel at b=64:
+    same bits as the explicit algorithm."""
     rng = np.random.default_rng(1)
     c = (rng.standard_normal((32, 32, 128)) * 0.01).astype(np.float32)
     x = rng.standard_normal((12, 4096)).astype(np.float32)
     ya, _ = _run(dev, x, c, None, "float32", "float32", algo="auto")
-    ys, _ = _run(dev, x, c, None, "float32", "float32", algo="stationary")
+    yd, _ = _run(dev, x, c, None, "float32", "float32", algo="dft")
+    assert torch.equal(ya, yd)
+    c64 = (rng.standard_normal((64, 64, 64)) * 0.01).astype(np.float32)
+    ya, _ = _run(dev, x, c64, None, "float32", "float32", algo="auto")
+    ys, _ = _run(dev, x, c64, None, "float32", "float32", algo="stationary")
     assert torch.equal(ya, ys)
 
 
