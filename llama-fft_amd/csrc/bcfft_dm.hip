@@ -74,10 +74,21 @@ __device__ __forceinline__ uint32_t pk_rne(float a, float b) {
 }
 __device__ __forceinline__ float lo16(uint32_t p) { return (float)__builtin_bit_cast(f16x2, p).x; }
 __device__ __forceinline__ float hi16(uint32_t p) { return (float)__builtin_bit_cast(f16x2, p).y; }
+// a - f32(fp16 half of h): one v_fma_mix_f32 (hipcc emits a conversion and a subtraction)
+__device__ __forceinline__ float sub_lo16(float a, uint32_t h) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(r) : "v"(a), "v"(h));
+  return r;
+}
+__device__ __forceinline__ float sub_hi16(float a, uint32_t h) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(r) : "v"(a), "v"(h));
+  return r;
+}
 // (a, b) -> fp16 hi (toward zero) and lo = the rest (toward zero)
 __device__ __forceinline__ void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
   hi = pk_rtz(a, b);
-  lo = pk_rtz(__builtin_fmaf(a, 1.f, -lo16(hi)), __builtin_fmaf(b, 1.f, -hi16(hi)));   // v_fma_mix
+  lo = pk_rtz(sub_lo16(a, hi), sub_hi16(b, hi));
 }
 // max |v| over the wave as an integer max of the magnitude bits (no NaN canonicalisation)
 __device__ __forceinline__ uint32_t wave_umax(uint32_t v) {
@@ -167,7 +178,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
   };
 
   // ---- prologue: first tile's x (I waves), the DFT table, the stationary B fragments
-  if (!fwave && wg_in_grp < n_mtiles) dma_token(wg_in_grp, lds, 0, NDMA);
+  if (fwave && wg_in_grp < n_mtiles) dma_token(wg_in_grp, lds, 0, NDMA);
   {
     const uint4* tab = reinterpret_cast<const uint4*>(kDmF);
 #pragma unroll
@@ -188,12 +199,30 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
           creg[fb][ks][nt] = __builtin_bit_cast(f16x8, img[((fb * KS + ks) * NT + nt) * 64]);
+    // pin the loads here: without a use, hipcc sinks them to their first use inside the tile loop
+    // and keeps counting them there (vmcnt(29..0) before each stage-2 MFMA), which then waits for
+    // every in-flight x DMA and y store of the iteration
+#pragma unroll
+    for (int fb = 0; fb < BW; ++fb)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(creg[fb][ks][nt]));
   }
   wait_vmcnt<0>();
   lds_barrier();
+#if defined(BCFFT_DM_PRIO) && BCFFT_DM_PRIO == 1          // experiment: I waves win arbitration
+  if (!fwave) __builtin_amdgcn_s_setprio(1);
+#elif defined(BCFFT_DM_PRIO) && BCFFT_DM_PRIO == 2        // experiment: F waves win arbitration
+  if (fwave) __builtin_amdgcn_s_setprio(1);
+#endif
 
   // ---- stage 1 (F wave, token slot s = wave): x rows -> X hi/lo units, in place, per half
   auto stage1 = [&](char* region, int par) {
+#if defined(BCFFT_DM_MEMONLY) || (defined(BCFFT_DM_ABL) && (BCFFT_DM_ABL & 1))   // analysis builds
+    if (lane < 2) wsc[par * 8 + wave * 2 + lane] = 0;
+    return;
+#endif
     const int l = opaque(lane);
     const int b16 = l & 15, g = l >> 4;
     char* slot = region + wave * SLOT;
@@ -237,14 +266,15 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
           }
         }
       SUBSTAMP(55 + 4 * hh);
-      uint32_t mx = 0u;                             // max |x| as magnitude bits
+      float mxf = 0.f;                              // max |x| (v_max3_f32 with |.| modifiers)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int pt = 0; pt < 2; ++pt)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) mx = max(mx, __float_as_uint(xv8[ks][pt][j]) & 0x7fffffffu);
-      const int sx = stat_scale_exp(2.f * __uint_as_float(wave_umax(mx)));   // |a|, |d| <= 2 max|x|
+          for (int j = 0; j < 8; ++j) mxf = __builtin_fmaxf(mxf, __builtin_fabsf(xv8[ks][pt][j]));
+      // across lanes as magnitude bits: no NaN canonicalisation around the DPP moves
+      const int sx = stat_scale_exp(2.f * __uint_as_float(wave_umax(__float_as_uint(mxf))));   // |a|, |d| <= 2 max|x|
       if (l == 0) wsc[par * 8 + wave * 2 + h] = sx - 7;     // X = D 2^-(sx - 7): the table's 2^-7
       const float S = __int_as_float((sx + 127) << 23);
       SUBSTAMP(56 + 4 * hh);
@@ -256,10 +286,11 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
         uint32_t ah[4], al[4], dh[4], dl[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float a0 = (xv8[ks][0][2 * e] + xv8[ks][1][2 * e]) * S;
-          const float a1 = (xv8[ks][0][2 * e + 1] + xv8[ks][1][2 * e + 1]) * S;
-          const float d0 = (xv8[ks][0][2 * e] - xv8[ks][1][2 * e]) * S;
-          const float d1 = (xv8[ks][0][2 * e + 1] - xv8[ks][1][2 * e + 1]) * S;
+          // a S = x_t S + x_{t+64} S, d S = x_t S - x_{t+64} S: exact power-of-two scale, so the
+          // fused forms round like (x_t +- x_{t+64}) S
+          const float u0 = xv8[ks][1][2 * e] * S, u1 = xv8[ks][1][2 * e + 1] * S;
+          const float a0 = fmaf(xv8[ks][0][2 * e], S, u0), a1 = fmaf(xv8[ks][0][2 * e + 1], S, u1);
+          const float d0 = fmaf(xv8[ks][0][2 * e], S, -u0), d1 = fmaf(xv8[ks][0][2 * e + 1], S, -u1);
           split2(a0, a1, ah[e], al[e]);
           split2(d0, d1, dh[e], dl[e]);
         }
@@ -303,6 +334,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
   // ---- stage 2 (all waves): per-bin complex MAC on bins f = 8 wave + fb; Y units over the
   // wave's own K-step-0 X units (the wave's DS operations execute in order)
   auto stage2 = [&](char* region, int par) {
+#if defined(BCFFT_DM_MEMONLY) || (defined(BCFFT_DM_ABL) && (BCFFT_DM_ABL & 2))
+    return;
+#endif
     const int ml = opaque(lane);
     const int arow = ml & 15, kb = ml >> 4;
     const int a_t = arow >> 2, a_reim = (arow >> 1) & 1, a_prec = arow & 1;
@@ -379,12 +413,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
   };
 
   // ---- stage 3 (I wave, token slot j = wave - 4 of the previous tile): Y -> y rows staged in
-  // LDS and stored as 1 KiB contiguous buffer stores. The slot's Y units (first 8 KiB) are read
-  // into registers first; its K-step-1 X units (second 8 KiB) are dead after stage 2. 16-bit y:
-  // 32 rows x 256 B staged in the second 8 KiB, and the next tile's x (8 KiB) comes in by
-  // LDS-DMA over the first 8 KiB at once. fp32 y: N-tile 0's rows in the second 8 KiB, N-tile
-  // 1's in the first, and the next x (16 KiB) follows the read-back.
-  auto stage3 = [&](char* region, int par, int64_t mp, int64_t mn) {
+  // the slot and stored as 1 KiB contiguous buffer stores. The slot's Y units are read into
+  // registers first. 16-bit y: 32 rows x 256 B in the second 8 KiB; fp32 y: N-tile 0's 16 rows
+  // in the second 8 KiB, N-tile 1's in the first. (The next tile's x arrives in P2.)
+  auto stage3 = [&](char* region, int par, int64_t mp) {
     const int l = opaque(lane);
     const int o16 = l & 15, g = l >> 4;
     char* slot = region + tslot * SLOT;
@@ -420,14 +452,13 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     gload(0, gcur);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // Y is in registers: the slot is free
     SUBSTAMP(55);
-    const bool dma = mn < n_mtiles;
-    if (ES == 2 && dma) dma_token(mn, region, 0, NDMA);
     SUBSTAMP(56);
     const int64_t tok = mp * TT + tslot;
     const bool tok_ok = tok < n_tokens;
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
         (char*)yv + (tok_ok ? tok : 0) * M * ESY, 0, tok_ok ? (int)(M * ESY) : 0, 0x00020000);
     const int nvalid = n_out - grp_o * NOG;
+#if !defined(BCFFT_DM_MEMONLY) && !(defined(BCFFT_DM_ABL) && (BCFFT_DM_ABL & 4))
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       if (!YSP_PREF_OFF && mt < 3) gload(mt + 1, gnxt);
@@ -450,14 +481,14 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const int o = 16 * nt + o16;
+        float os[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) os[r] = O[nt][r] * ysc;
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
           float v[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float os = O[nt][r] * ysc;
-            v[r] = hf ? fmaf(E[nt][r], ysc, -os) : fmaf(E[nt][r], ysc, os);
-          }
+          for (int r = 0; r < 4; ++r) v[r] = hf ? fmaf(E[nt][r], ysc, -os[r]) : fmaf(E[nt][r], ysc, os[r]);
           if (Y32 || bias_dt != BCFFT_NONE) {       // .to(x dtype) :266, + bias :270-271
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = round_to(v[r], XT);
@@ -490,6 +521,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
         }
       }
     }
+#endif
     SUBSTAMP(57);
     // staged rows -> global: each instruction stores 1 KiB = RPI whole y rows of the group
     constexpr int RB = B * ESY, RPI = 1024 / RB, LPR = 64 / RPI;   // row bytes, rows/store, lanes/row
@@ -518,19 +550,15 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
       }
     }
     SUBSTAMP(58);
-    if constexpr (ES == 4) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // staged rows read back: slot free
-      if (dma) dma_token(mn, region, 0, NDMA);
-    }
-    SUBSTAMP(59);
   };
 
   // Pipeline, two workgroup barriers per M-tile. Iteration it (region R = it & 1 holds tile m,
   // the other R' tile m - gstride):
-  //   P1  F waves: stage 1 of tile m in R.  I waves: stage 3 of tile m - gstride from R' (its
-  //       Y read first, then the LDS-DMA of x(m + gstride) into the freed slot of R', then
-  //       the y stores)                                                            | Ba |
-  //   P2  all waves: stage 2 of tile m in R; I waves then wait for their DMA       | Bb |
+  //   P1  F waves: wait for their own x DMA, stage 1 of tile m in R.  I waves: stage 3 of tile
+  //       m - gstride from R' (Y read, y staged in the slot, 1 KiB stores)          | Ba |
+  //   P2  F waves: LDS-DMA of x(m + gstride) into their slot of R'; all waves: stage 2 of
+  //       tile m in R                                                               | Bb |
+  // so the tile's HBM traffic is split between the phases: y stores in P1, x loads in P2.
   int64_t m = wg_in_grp;
   STAMP(0);
   for (int it = 0; m < n_mtiles || it > 0; ++it, m += gstride) {
@@ -542,21 +570,24 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     sub_on = it == 4;
     STAMP(sb);
     if (fwave) {
-      if (have_f) stage1(region, par);
+      if (have_f) {
+        wait_vmcnt<0>();                            // this wave's own x DMA (issued a phase ahead)
+        stage1(region, par);
+      }
     } else if (it > 0) {
-      stage3(other, par ^ 1, m - gstride, m + gstride);
-    } else if (m + gstride < n_mtiles) {
-      dma_token(m + gstride, other, 0, NDMA);
+      stage3(other, par ^ 1, m - gstride);
     }
     STAMP(sb + 1);
     if (!have_f) break;
     lds_barrier();                                  // Ba: X units and scales complete
     STAMP(sb + 2);
-    stage2(region, par);
+    // F wave j streams the next tile's x for its slot j of the other region: stage 3 has read
+    // that slot's Y and staged y (each wave's LDS reads completed before Ba)
+    if (fwave && m + gstride < n_mtiles) dma_token(m + gstride, other, 0, NDMA);
     STAMP(sb + 3);
-    if (!fwave) wait_vmcnt<0>();                    // the next tile's x has landed (and the stores)
+    stage2(region, par);
     STAMP(sb + 4);
-    lds_barrier();                                  // Bb: Y units complete, x(m + gstride) staged
+    lds_barrier();                                  // Bb: Y units complete
     STAMP(sb + 5);
   }
   STAMP(63);
@@ -583,7 +614,7 @@ void launch_dm(const void* x, int64_t n, int n_out, const void* spec, const void
 #if defined(BCFFT_ABLATE) || defined(BCFFT_STAMPS)
 // analysis builds only: stamp buffer of bc_forward_dm_kernel (this TU's copy). Slots per wave:
 // 0 start | per M-tile it (base 1 + 6 min(it, 8)): +0 loop top, +1 stage 1 / stage 3 done,
-// +2 after Ba, +3 stage 2 done, +4 DMA landed (I waves), +5 after Bb | 55-62 sub-phases of
+// +2 after Ba, +3 DMA issued (F waves), +4 stage 2 done, +5 after Bb | 55-62 sub-phases of
 // iteration 4 (F waves, per half: x read, scale, MFMAs, X written; I waves: Y read, DMA issued,
 // per N-tile computed + stored, DMA 2 issued) | 63 end
 extern "C" int bcfft_set_stamps_dm(void* buf) {

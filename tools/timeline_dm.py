@@ -1,7 +1,7 @@
 """Phase timeline of the DFT-on-MFMA kernel (analysis build only: lib/libbcfft_stamps.so from
 `make -C llama-fft_amd stamps`, the product's control flow with s_memtime stamps). Slots per wave
 (bcfft_dm.hip): 0 start | per M-tile it (base 1 + 6 min(it, 8)): +0 loop top, +1 stage 1 (F waves
-0-3) / stage 3 + DMA issue (I waves 4-7) done, +2 after barrier Ba, +3 stage 2 done, +4 DMA landed,
+0-3) / stage 3 + DMA issue (I waves 4-7) done, +2 after barrier Ba, +3 x DMA issued (F waves), +4 stage 2 done,
 +5 after Bb | 55-62 sub-phases of iteration 4 | 63 end. Prints per-wave-class medians of the segments in cycles.
 usage: python tools/timeline_dm.py [M IO N]"""
 import ctypes
@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.join(ROOT, "llama-fft_amd"))
 import torch  # noqa: E402
 from bcfft import _lib, ops  # noqa: E402
 
-SEG = ["P1 work", "Ba wait", "stage2", "dma wait", "Bb wait"]
+SEG = ["P1 work", "Ba wait", "dma issue", "stage2", "Bb wait"]
 
 
 def run(m, io, n, k=4096, b=128):
@@ -67,7 +67,7 @@ def run(m, io, n, k=4096, b=128):
     if tiles > 4:                                # sub-phases of iteration 4 (from its loop top)
         top = st[:, 1 + 6 * 4]
         fsub = ["x read h0", "scale h0", "mfma h0", "X wr h0", "x read h1", "scale h1", "mfma h1", "X wr h1"]
-        isub = ["Y+G read", "DMA16 issue", "compute", "stores", "DMA32 issue", "-", "-", "-"]
+        isub = ["Y+G read", "-", "compute", "stores", "-", "-", "-", "-"]
         for name, sel, lab in (("F", wv < 4, fsub), ("I", wv >= 4, isub)):
             prev = top[sel]
             out = []
