@@ -51,10 +51,14 @@ def resolved_kernel(algo, k, b):
     n_in = k // b
     stat_ok = (b == 128 and n_in == 32) or (b == 64 and n_in in (32, 64))
     dft_ok = b == 128 and n_in == 32
+    if algo == "dftx":
+        return ("dftx", "bc_forward_dm_kernel",
+                "MFMA fp16 throughout: block DFT (even/odd split, x hi+lo) x 2^-7 table, stationary "
+                "conj(C)*s_C MAC (X hi+lo), inverse DFT of Y hi+lo; f32 accumulate")
     if algo == "dft" or (algo == "auto" and dft_ok):
         return ("dft", "bc_forward_dm_kernel",
                 "MFMA fp16 throughout: block DFT (even/odd split, x hi+lo) x 2^-7 table, stationary "
-                "conj(C)*s_C MAC (X hi+lo), inverse DFT; f32 accumulate")
+                "conj(C)*s_C MAC (X hi+lo), inverse DFT (Y one fp16 term); f32 accumulate")
     if algo == "stationary" or (algo == "auto" and stat_ok):
         return ("stationary", "bc_forward_stat_kernel",
                 "MFMA fp16: conj(C)*s_C (VGPR-resident) x per-token-scaled X split hi+lo, f32 accumulate")
@@ -156,15 +160,16 @@ def time_glu(dev, steps, k=4096, m=11008, b=128, n=8192, io="bf16"):
             "frac": round(nbytes / (fused * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
-def load_traffic(tag):
-    """Per-launch HBM bytes from the newest profiles/pmc_traffic_*.json for this workload."""
+def load_traffic(tag, kernel):
+    """Per-launch HBM bytes of this kernel on this workload from the newest
+    profiles/pmc_traffic_*.json that measured that pair (None if none did)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic_*.json")))
     for f in reversed(files):
         try:
             d = json.load(open(f))
         except Exception:
             continue
-        if tag in d:
+        if tag in d and d[tag].get("kernel") == kernel:
             return d[tag].get("hbm_bytes_per_launch")
     return None
 
@@ -237,6 +242,7 @@ def main():
         # the north star in bf16 and on the other engines, and the config-4 sweep b x shape (bf16)
         vlist = [(4096, 4096, 64, "fp32", 128, "auto"),
                  (4096, 4096, 128, "bf16", 8192, "auto"),
+                 (4096, 4096, 128, "fp32", 8192, "dftx"),
                  (4096, 4096, 128, "fp32", 8192, "stationary"),
                  (4096, 4096, 128, "bf16", 8192, "stationary"),
                  (4096, 4096, 128, "fp32", 8192, "mfma"),
@@ -331,7 +337,7 @@ def main():
                        "algo": algo, "algo_resolved": kname[0], "mac": kname[2]},
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
-                         "traffic": load_traffic(tag),
+                         "traffic": load_traffic(tag, kname[1]),
                          "kernel": kname[1], "kernel_ms": round(kern, 5),
                          "algorithmic_bytes_per_launch": nbytes,
                          "fp32_tflops": round(algo_flops(n, k, m, b) / (kern * 1e-3) / 1e12, 2),

@@ -45,10 +45,13 @@ enum bcfft_dtype { BCFFT_NONE = -1, BCFFT_F32 = 0, BCFFT_F16 = 1, BCFFT_BF16 = 2
  *  VALU: per-bin complex MAC in fp32 FMAs (the reference's fp32 arithmetic). Any block size.
  *  DFT:  the STAT weights, with the forward and inverse DFTs of the blocks also on the matrix
  *        cores (dense fp16 GEMMs against a 2^-7-scaled DFT table, even/odd split) instead of
- *        VALU FFTs; ~3.5e-4 relative. Geometry: block_size 128 with in_features 4096.
+ *        VALU FFTs; ~3.5e-4 relative (fp16 outputs: as DFTX). Geometry: block_size 128 with
+ *        in_features 4096.
+ *  DFTX: DFT with the per-bin products also split hi + lo before the inverse transform:
+ *        ~2.8e-4 relative and linear in x to ~1e-6, ~6 % slower.
  *  AUTO: DFT where eligible, else STAT where eligible, else MFMA for block_size <= 128, else VALU. */
 enum bcfft_algo { BCFFT_ALGO_AUTO = 0, BCFFT_ALGO_MFMA = 1, BCFFT_ALGO_VALU = 2, BCFFT_ALGO_STAT = 3,
-                  BCFFT_ALGO_DFT = 4 };
+                  BCFFT_ALGO_DFT = 4, BCFFT_ALGO_DFTX = 5 };
 
 enum bcfft_status {
   BCFFT_OK = 0,

@@ -97,7 +97,7 @@ def glu_eligible(in_features: int, block_size: int) -> bool:
 
 
 def default_algo() -> str:
-    """BCFFT_ALGO env var: auto (default) | dft | stationary | mfma | valu."""
+    """BCFFT_ALGO env var: auto (default) | dft | dftx | stationary | mfma | valu."""
     import os
     a = os.environ.get("BCFFT_ALGO", "auto").lower()
     if a not in _lib.ALGOS:
@@ -109,7 +109,8 @@ def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, bl
             out_features: int, algo: str | None = None) -> torch.Tensor:
     """y = BC(x2d) (+ bias) with one fused kernel. x2d: (N, K) device tensor.
     algo: "auto" (dft where eligible, else stationary where eligible, else mfma for b <= 128,
-    else valu), "dft" (block DFTs and MAC on fp16 MFMA, weights in VGPRs, ~3.5e-4),
+    else valu), "dft" (block DFTs and MAC on fp16 MFMA, weights in VGPRs, ~3.5e-4), "dftx"
+    (dft with the per-bin products split hi + lo: ~2.8e-4, linear to ~1e-6),
     "stationary" (weights in VGPRs, fp16 MFMA, ~3e-4), "mfma" (split-bf16, ~1e-5) or
     "valu" (exact fp32 MAC). See include/bcfft.h."""
     _lib.require_device(x2d, "bcfft.forward")

@@ -503,7 +503,7 @@ bool launch_forward_glu(int b, int n_in, int xdt, const void* x, int64_t n, int 
 void launch_stat_image(int b, int n_out, int n_in, void* spec, hipStream_t s);
 // DFT-on-MFMA kernel (bcfft_dm.hip): the STAT image's geometry subset b = 128, K = 4096
 bool dm_eligible(int n_in, int b);
-bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, const void* x, int64_t n, int n_out,
+bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, bool exact, const void* x, int64_t n, int n_out,
                        const void* spec, const void* bias, int bias_dt, void* y, hipStream_t s);
 
 // weight prep (bcfft_prep.hip): loss-aware circulant projection of a dense (n_out*b, n_in*b)

@@ -18,10 +18,11 @@
 //    LDS-DMA; then all 8 waves run the per-bin complex MAC (stage 2) on their 8 bins, exactly as
 //    the stationary kernel. Two workgroup barriers per M-tile, two 64 KiB LDS regions.
 //  * Numerics: a, d split into fp16 hi + lo under a per-(token, 16-block half) power-of-two
-//    scale; X split into hi + lo; Y split into hi + lo (a fixed 2^-21 keeps it in range;
-//    BCFFT_DM_YSPLIT=0 builds one RNE term: ~10 % faster, ~3.5e-4); C and the table one fp16
-//    term each; fp32 accumulation everywhere: ~2.8e-4 relative on the layer output, linear in x
-//    to ~1e-6 (tests/dm_model.py restates it; north star: 1e-3).
+//    scale; X split into hi + lo; C and the table one fp16 term each; Y (a fixed 2^-21 keeps it
+//    in range) one RNE fp16 term (~3.5e-4 relative on the layer output; the default) or, with
+//    YSP (BCFFT_ALGO_DFTX, and always for fp16 outputs, whose ulp is close to that noise), hi +
+//    lo (~2.8e-4, linear in x to ~1e-6; ~6 % slower); fp32 accumulation everywhere
+//    (tests/dm_model.py restates both; north star: 1e-3).
 //
 // Geometry: b = 128 with K = 4096 (32 input blocks: two K-steps of 16), any M (output groups of
 // 32 blocks), x fp32 / fp16 / bf16, y = promote(x, bias). LDS and register maps below; every
@@ -29,9 +30,6 @@
 #include "bcfft_device.h"
 #include "bcfft_dm_table.h"
 
-#ifndef BCFFT_DM_YSPLIT
-#define BCFFT_DM_YSPLIT 1                   // Y as fp16 hi + lo (else one RNE term)
-#endif
 
 namespace bcfft {
 
@@ -105,7 +103,7 @@ __device__ __forceinline__ f16x8 frag(uint32_t a, uint32_t b, uint32_t c, uint32
 }
 }  // namespace dmk
 
-template <int XT, bool YF32>
+template <int XT, bool YF32, bool YSP>
 __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_out, const uint32_t* __restrict__ stat,
     const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
@@ -333,8 +331,11 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
 
   // ---- stage 2 (all waves): per-bin complex MAC on bins f = 8 wave + fb; Y units over the
   // wave's own K-step-0 X units (the wave's DS operations execute in order)
-  auto stage2 = [&](char* region, int par) {
+  // dma_next: this F wave streams the next tile's x into its slot of `dregion`, a piece or two
+  // per bin (spreads the x traffic over the phase instead of one burst at its start)
+  auto stage2 = [&](char* region, int par, bool dma_next, int64_t mnext, char* dregion) {
 #if defined(BCFFT_DM_MEMONLY) || (defined(BCFFT_DM_ABL) && (BCFFT_DM_ABL & 2))
+    if (dma_next) dma_token(mnext, dregion, 0, NDMA);
     return;
 #endif
     const int ml = opaque(lane);
@@ -366,11 +367,11 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
         araw[fb][ks] = *reinterpret_cast<const uint4*>((fb < 4 ? ab0 : ab1) + 128 * fb + 8192 * ks);
-    constexpr bool YSP = BCFFT_DM_YSPLIT;
     uint32_t yh[BW][NT], yl[BW][NT];
 #pragma unroll
     for (int fb = 0; fb < BW; ++fb) {
       const int f = wave * BW + fb;
+      if (dma_next) dma_token(mnext, dregion, fb * (NDMA / BW), (fb + 1) * (NDMA / BW));
       f32x4 acc[NT];
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -424,7 +425,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     const int nmin = min(sc[0], sc[1]);
     const float ysc = __builtin_ldexpf(inv_sc, 30 - nmin);
     // all Y fragments of the token: B[k = 8 g + j][o] = unit(wave 4 ks + g, o, parity)
-    constexpr bool YSP = BCFFT_DM_YSPLIT;
     constexpr int NYP = YSP ? 2 : 1;                // Y precision terms (hi; lo 8 KiB further)
     constexpr bool YSP_PREF_OFF = YSP;              // the lo terms take the table prefetch's VGPRs
     uint4 yf[NYP][KS][2][NT];
@@ -577,15 +577,34 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     } else if (it > 0) {
       stage3(other, par ^ 1, m - gstride);
     }
+#if defined(BCFFT_DM_DMAP1)
+    if (!fwave && m + gstride < n_mtiles) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      dma_token(m + gstride, other, 0, NDMA);
+    }
+#endif
     STAMP(sb + 1);
     if (!have_f) break;
     lds_barrier();                                  // Ba: X units and scales complete
     STAMP(sb + 2);
     // F wave j streams the next tile's x for its slot j of the other region: stage 3 has read
     // that slot's Y and staged y (each wave's LDS reads completed before Ba)
+#if defined(BCFFT_DM_DMASPLIT)                    // experiment: F and I waves each issue half
+    if (m + gstride < n_mtiles) dma_token(m + gstride, other, fwave ? 0 : NDMA / 2, fwave ? NDMA / 2 : NDMA);
+    const bool dma2 = false;
+#elif defined(BCFFT_DM_DMAP1)                       // experiment: I waves issue it at the end of P1
+    const bool dma2 = false;
+#elif defined(BCFFT_DM_DMAINTER)                    // experiment: pieces between the stage-2 bins
+    const bool dma2 = fwave && m + gstride < n_mtiles;
+#else                                               // one burst at the start of phase 2 (measured best)
     if (fwave && m + gstride < n_mtiles) dma_token(m + gstride, other, 0, NDMA);
+    const bool dma2 = false;
+#endif
     STAMP(sb + 3);
-    stage2(region, par);
+    stage2(region, par, dma2, m + gstride, other);
+#if defined(BCFFT_DM_DMASPLIT) || defined(BCFFT_DM_DMAP1)
+    if (!fwave) wait_vmcnt<0>();                    // their share of the next x has landed
+#endif
     STAMP(sb + 4);
     lds_barrier();                                  // Bb: Y units complete
     STAMP(sb + 5);
@@ -596,7 +615,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
 }  // namespace bcfft
 
 namespace {
-template <int XT, bool YF32>
+template <int XT, bool YF32, bool YSP>
 void launch_dm(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt, void* y,
                hipStream_t s) {
   const int groups = (n_out + 31) / 32;
@@ -606,7 +625,7 @@ void launch_dm(const void* x, int64_t n, int n_out, const void* spec, const void
   if (total > groups * n_mtiles) total = groups * n_mtiles;
   if (total < groups) total = groups;
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
-  hipLaunchKernelGGL((bcfft::bc_forward_dm_kernel<XT, YF32>), dim3((unsigned)total), dim3(512), 0, s, x, n,
+  hipLaunchKernelGGL((bcfft::bc_forward_dm_kernel<XT, YF32, YSP>), dim3((unsigned)total), dim3(512), 0, s, x, n,
                      n_out, stat, bias, bias_dt, y);
 }
 }  // namespace
@@ -626,14 +645,19 @@ extern "C" int bcfft_set_stamps_dm(void* buf) {
 namespace bcfft {
 bool dm_eligible(int n_in, int b) { return b == 128 && n_in == 32; }
 
-bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, const void* x, int64_t n, int n_out,
+// exact: Y as hi + lo (BCFFT_ALGO_DFTX); fp16 outputs always take it
+bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, bool exact, const void* x, int64_t n, int n_out,
                        const void* spec, const void* bias, int bias_dt, void* y, hipStream_t s) {
   if (!dm_eligible(n_in, b)) return false;
-  if (xdt == BCFFT_F32) launch_dm<BCFFT_F32, true>(x, n, n_out, spec, bias, bias_dt, y, s);
-  else if (xdt == BCFFT_F16 && yf32) launch_dm<BCFFT_F16, true>(x, n, n_out, spec, bias, bias_dt, y, s);
-  else if (xdt == BCFFT_F16) launch_dm<BCFFT_F16, false>(x, n, n_out, spec, bias, bias_dt, y, s);
-  else if (yf32) launch_dm<BCFFT_BF16, true>(x, n, n_out, spec, bias, bias_dt, y, s);
-  else launch_dm<BCFFT_BF16, false>(x, n, n_out, spec, bias, bias_dt, y, s);
+#define BCFFT_DM_LAUNCH(XT, YF)                                                      \
+  (exact ? launch_dm<XT, YF, true>(x, n, n_out, spec, bias, bias_dt, y, s)          \
+         : launch_dm<XT, YF, false>(x, n, n_out, spec, bias, bias_dt, y, s))
+  if (xdt == BCFFT_F32) BCFFT_DM_LAUNCH(BCFFT_F32, true);
+  else if (xdt == BCFFT_F16 && yf32) BCFFT_DM_LAUNCH(BCFFT_F16, true);
+  else if (xdt == BCFFT_F16) launch_dm<BCFFT_F16, false, true>(x, n, n_out, spec, bias, bias_dt, y, s);
+  else if (yf32) BCFFT_DM_LAUNCH(BCFFT_BF16, true);
+  else BCFFT_DM_LAUNCH(BCFFT_BF16, false);
+#undef BCFFT_DM_LAUNCH
   return true;
 }
 }  // namespace bcfft

@@ -768,7 +768,7 @@ int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_featur
   if (y_dtype != promote(x_dtype, bias_dtype)) return BCFFT_ERR_DTYPE;
   if ((bias == nullptr) != (bias_dtype == BCFFT_NONE)) return BCFFT_ERR_ARG;
   if (algo != BCFFT_ALGO_AUTO && algo != BCFFT_ALGO_MFMA && algo != BCFFT_ALGO_VALU &&
-      algo != BCFFT_ALGO_STAT && algo != BCFFT_ALGO_DFT)
+      algo != BCFFT_ALGO_STAT && algo != BCFFT_ALGO_DFT && algo != BCFFT_ALGO_DFTX)
     return BCFFT_ERR_ARG;
   if (n_tokens == 0) return BCFFT_OK;
   if (!x || !y || !spectra) return BCFFT_ERR_ARG;
@@ -778,15 +778,16 @@ int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_featur
   const int n_in = in_features / block_size, n_out = out_features / block_size;
   const bool stat_ok = bcfft::stat_eligible(n_in, block_size);
   if (algo == BCFFT_ALGO_STAT && !stat_ok) return BCFFT_ERR_BLOCK;
-  if (algo == BCFFT_ALGO_DFT && !bcfft::dm_eligible(n_in, block_size)) return BCFFT_ERR_BLOCK;
+  if ((algo == BCFFT_ALGO_DFT || algo == BCFFT_ALGO_DFTX) && !bcfft::dm_eligible(n_in, block_size))
+    return BCFFT_ERR_BLOCK;
   algo = resolve_algo(algo, n_in, block_size);
   // the workspace is used only when it is as large as bcfft_forward_workspace_bytes asks
   const int64_t need = bcfft_forward_workspace_bytes(n_tokens, in_features, out_features, block_size, algo);
   float* ws = (workspace && need > 0 && workspace_bytes >= need) ? (float*)workspace : nullptr;
   hipStream_t s = (hipStream_t)stream;
-  if (algo == BCFFT_ALGO_DFT) {
-    bcfft::launch_forward_dm(block_size, n_in, x_dtype, y_dtype == BCFFT_F32, x, n_tokens, n_out, spectra, bias,
-                             bias_dtype, y, s);
+  if (algo == BCFFT_ALGO_DFT || algo == BCFFT_ALGO_DFTX) {
+    bcfft::launch_forward_dm(block_size, n_in, x_dtype, y_dtype == BCFFT_F32, algo == BCFFT_ALGO_DFTX, x, n_tokens,
+                             n_out, spectra, bias, bias_dtype, y, s);
     return record_launch();
   }
   if (algo == BCFFT_ALGO_STAT) {

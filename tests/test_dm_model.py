@@ -17,7 +17,7 @@ def test_table_matches_dft():
     assert np.allclose(F[:, 64 + 2 * 5 + 1], -np.sin(2 * np.pi * 11 * t / 128), atol=1e-3)
 
 
-@pytest.mark.parametrize("scale,ysplit", [(1.0, True), (1e-5, True), (3e4, True), (1.0, False)])
+@pytest.mark.parametrize("scale,ysplit", [(1.0, True), (1e-5, True), (3e4, True), (1.0, False), (1e-5, False), (3e4, False)])
 def test_dm_model_vs_oracle(scale, ysplit):
     rng = np.random.default_rng(7)
     x = (rng.standard_normal((6, 4096)) * scale).astype(np.float32)

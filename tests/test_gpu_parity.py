@@ -178,8 +178,14 @@ def test_north_star_full_size_vs_oracle(dev, monkeypatch, algo):
     assert e < (2e-6 if algo == "valu" else 5e-5), e
 
 
-def test_linearity_full_size(dev):
+@pytest.mark.parametrize("algo,tol", [
+    ("auto", 1e-3),        # dft: the per-bin products rounded once to fp16 (~3e-4 noise per call)
+    ("dftx", 1e-5),        # products split hi + lo: linear to ~1e-6
+    ("stationary", 1e-5),
+])
+def test_linearity_full_size(dev, monkeypatch, algo, tol):
     """BC(a x1 + x2) = a BC(x1) + BC(x2) at the bench shape (size-independent property)."""
+    monkeypatch.setenv("BCFFT_ALGO", algo)
     torch.manual_seed(0)
     from patch_llama_fft import BlockCirculantLinear
     mod = BlockCirculantLinear(4096, 11008, block_size=128, bias=False).to(dev).eval()
@@ -188,7 +194,7 @@ def test_linearity_full_size(dev):
     with torch.no_grad():
         lhs = mod(2.5 * x1 + x2)
         rhs = 2.5 * mod(x1) + mod(x2)
-    assert (lhs - rhs).norm() / rhs.norm() < 1e-5
+    assert (lhs - rhs).norm() / rhs.norm() < tol
 
 
 def test_spectra_cache_invalidation(dev):

@@ -16,16 +16,19 @@ def t_one(k, m, b, io, algo, n=8192, iters=50):
     c = (torch.randn(m // b, k // b, b) * 0.01).cuda()
     spec = ops.spectra(c)
     x = torch.randn(n, k, device="cuda").to(DT[io])
-    for _ in range(5):
+    for _ in range(150):                            # ~10 ms: clocks settle before timing
         ops.forward(x, spec, None, b, m, algo=algo)
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    s.record()
-    for _ in range(iters):
-        ops.forward(x, spec, None, b, m, algo=algo)
-    e.record()
-    torch.cuda.synchronize()
-    us = s.elapsed_time(e) / iters * 1e3
+    reps = []
+    for _ in range(5):                              # median of 5 repeats
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(iters):
+            ops.forward(x, spec, None, b, m, algo=algo)
+        e.record()
+        torch.cuda.synchronize()
+        reps.append(s.elapsed_time(e) / iters * 1e3)
+    us = sorted(reps)[2]
     es = 4 if io == "fp32" else 2
     nbytes = n * k * es + n * m * es + (m // b) * (k // b) * (b // 2 + 1) * 8
     print(f"{algo:10s} {k}x{m} b{b} {io} N={n}: {us:8.1f} us  {nbytes / us / 1e3:7.1f} GB/s  "
