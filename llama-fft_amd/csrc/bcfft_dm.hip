@@ -17,11 +17,11 @@
 //    (I) inverse-transform token w-4 of the previous tile (stage 3) and stream the next x in by
 //    LDS-DMA; then all 8 waves run the per-bin complex MAC (stage 2) on their 8 bins, exactly as
 //    the stationary kernel. Two workgroup barriers per M-tile, two 64 KiB LDS regions.
-//  * Numerics: a, d split into fp16 hi + lo under a per-(token, 16-block half) power-of-two
-//    scale; X split into hi + lo; C and the table one fp16 term each; Y (a fixed 2^-21 keeps it
-//    in range) one RNE fp16 term (~3.5e-4 relative on the layer output; the default) or, with
-//    YSP (BCFFT_ALGO_DFTX, and always for fp16 outputs, whose ulp is close to that noise), hi +
-//    lo (~2.8e-4, linear in x to ~1e-6; ~6 % slower); fp32 accumulation everywhere
+//  * Numerics: per-(token, 16-block half) power-of-two scales; X split into fp16 hi + lo; C and
+//    the table one fp16 term each; fp32 accumulation everywhere. a, d and the per-bin products Y
+//    (a fixed 2^-21 keeps Y in range) are one RNE fp16 term each (~4e-4 relative on the layer
+//    output; the default) or, in the exact variant EX (BCFFT_ALGO_DFTX, and always for fp16
+//    outputs, whose ulp is close to that noise), hi + lo (~2.8e-4, linear in x to ~1e-6)
 //    (tests/dm_model.py restates both; north star: 1e-3).
 //
 // Geometry: b = 128 with K = 4096 (32 input blocks: two K-steps of 16), any M (output groups of
@@ -103,7 +103,7 @@ __device__ __forceinline__ f16x8 frag(uint32_t a, uint32_t b, uint32_t c, uint32
 }
 }  // namespace dmk
 
-template <int XT, bool YF32, bool YSP>
+template <int XT, bool YF32, bool EX>
 __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_out, const uint32_t* __restrict__ stat,
     const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
@@ -289,11 +289,15 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
           const float u0 = xv8[ks][1][2 * e] * S, u1 = xv8[ks][1][2 * e + 1] * S;
           const float a0 = fmaf(xv8[ks][0][2 * e], S, u0), a1 = fmaf(xv8[ks][0][2 * e + 1], S, u1);
           const float d0 = fmaf(xv8[ks][0][2 * e], S, -u0), d1 = fmaf(xv8[ks][0][2 * e + 1], S, -u1);
-          split2(a0, a1, ah[e], al[e]);
-          split2(d0, d1, dh[e], dl[e]);
+          if constexpr (EX) {
+            split2(a0, a1, ah[e], al[e]);
+            split2(d0, d1, dh[e], dl[e]);
+          } else {                                  // one RNE fp16 term
+            ah[e] = pk_rne(a0, a1);
+            dh[e] = pk_rne(d0, d1);
+          }
         }
-        const f16x8 bah = frag(ah[0], ah[1], ah[2], ah[3]), bal = frag(al[0], al[1], al[2], al[3]);
-        const f16x8 bdh = frag(dh[0], dh[1], dh[2], dh[3]), bdl = frag(dl[0], dl[1], dl[2], dl[3]);
+        const f16x8 bah = frag(ah[0], ah[1], ah[2], ah[3]), bdh = frag(dh[0], dh[1], dh[2], dh[3]);
 #pragma unroll
         for (int pr = 0; pr < 2; ++pr)
 #pragma unroll
@@ -305,7 +309,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
             const s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p0 + 256 * 4));
             const f16x8 af = __builtin_bit_cast(f16x8, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
             acc[4 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, pr ? bdh : bah, acc[4 * pr + mt], 0, 0, 0);
-            acc[4 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, pr ? bdl : bal, acc[4 * pr + mt], 0, 0, 0);
+            if constexpr (EX) {
+              const f16x8 bal = frag(al[0], al[1], al[2], al[3]), bdl = frag(dl[0], dl[1], dl[2], dl[3]);
+              acc[4 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, pr ? bdl : bal, acc[4 * pr + mt], 0, 0, 0);
+            }
           }
       }
       // D^T tile (pr, mt): rows 4g + r = cols of bins fA = 16 mt + 4 g + pr (r = 0, 1: re, im)
@@ -397,7 +404,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
       for (int nt = 0; nt < NT; ++nt)                // rows 4 yt + {re hi, re lo, im hi, im lo}
       {
         const float yr = (acc[nt][0] + acc[nt][1]) * YS, yi = (acc[nt][2] + acc[nt][3]) * YS;
-        if constexpr (YSP) split2(yr, yi, yh[fb][nt], yl[fb][nt]);
+        if constexpr (EX) split2(yr, yi, yh[fb][nt], yl[fb][nt]);
         else yh[fb][nt] = pk_rne(yr, yi);
       }
     }
@@ -406,7 +413,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     for (int nt = 0; nt < NT; ++nt) {
       *reinterpret_cast<uint4*>(yb + 16 * 16 * nt) = make_uint4(yh[0][nt], yh[2][nt], yh[4][nt], yh[6][nt]);
       *reinterpret_cast<uint4*>(yb + 16 * (32 + 16 * nt)) = make_uint4(yh[1][nt], yh[3][nt], yh[5][nt], yh[7][nt]);
-      if constexpr (YSP) {                          // lo terms over the K-step-1 X units of these bins
+      if constexpr (EX) {                           // lo terms over the K-step-1 X units of these bins
         *reinterpret_cast<uint4*>(yb + 8192 + 16 * 16 * nt) = make_uint4(yl[0][nt], yl[2][nt], yl[4][nt], yl[6][nt]);
         *reinterpret_cast<uint4*>(yb + 8192 + 16 * (32 + 16 * nt)) = make_uint4(yl[1][nt], yl[3][nt], yl[5][nt], yl[7][nt]);
       }
@@ -425,8 +432,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     const int nmin = min(sc[0], sc[1]);
     const float ysc = __builtin_ldexpf(inv_sc, 30 - nmin);
     // all Y fragments of the token: B[k = 8 g + j][o] = unit(wave 4 ks + g, o, parity)
-    constexpr int NYP = YSP ? 2 : 1;                // Y precision terms (hi; lo 8 KiB further)
-    constexpr bool YSP_PREF_OFF = YSP;              // the lo terms take the table prefetch's VGPRs
+    constexpr int NYP = EX ? 2 : 1;                 // Y precision terms (hi; lo 8 KiB further)
+    constexpr bool YSP_PREF_OFF = EX;               // the lo terms take the table prefetch's VGPRs
     uint4 yf[NYP][KS][2][NT];
     const char* yb = slot + g * 1024 + 16 * o16;
 #pragma unroll
@@ -455,9 +462,21 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     SUBSTAMP(56);
     const int64_t tok = mp * TT + tslot;
     const bool tok_ok = tok < n_tokens;
-    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
-        (char*)yv + (tok_ok ? tok : 0) * M * ESY, 0, tok_ok ? (int)(M * ESY) : 0, 0x00020000);
     const int nvalid = n_out - grp_o * NOG;
+    // staging write bases (lane part of the XOR-swizzled address; the rest are immediates).
+    // fp32: (4 mt + g) ^ s = 4 mt + (g ^ (s & 3)) +- 4 (s >> 2) by the parity of mt (s = o16 & 7);
+    // 16-bit: (4 mt + g) ^ sg for each mt (sg = ((o16 & 7) << 1) | (o16 >> 3))
+    int swb[Y32 ? 2 : 4];
+    if constexpr (Y32) {
+      const int s7 = o16 & 7;
+      const int b0 = 512 * o16 + 16 * (g ^ (s7 & 3));
+      swb[0] = b0 + 64 * (s7 >> 2);
+      swb[1] = b0 - 64 * (s7 >> 2);
+    } else {
+      const int sg = ((o16 & 7) << 1) | (o16 >> 3);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) swb[mt] = 256 * o16 + 8 * ((4 * mt + g) ^ sg);
+    }
 #if !defined(BCFFT_DM_MEMONLY) && !(defined(BCFFT_DM_ABL) && (BCFFT_DM_ABL & 4))
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
@@ -498,14 +517,11 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
               for (int r = 0; r < 4; ++r) v[r] += load_scalar(bias, cc + r, bias_dt);
             }
           }
-          if constexpr (Y32) {                      // N-tile nt's 16 rows, 16-B unit u of row o16
-            char* stg = slot + (nt ? 0 : 8192);
-            const int u = 4 * mt + g + 16 * hf;
-            *reinterpret_cast<float4*>(stg + 512 * o16 + 16 * (u ^ (o16 & 7))) = make_float4(v[0], v[1], v[2], v[3]);
-          } else {                                  // row o of the 32, 8-B unit v8
-            const int v8 = 4 * mt + g + 16 * hf;
-            const int sg = ((o & 7) << 1) | ((o >> 3) & 1);
-            *reinterpret_cast<uint2*>(slot + 8192 + 256 * o + 8 * (v8 ^ sg)) =
+          if constexpr (Y32) {                      // N-tile nt's 16 rows: unit (4 mt + g + 16 hf) ^ (o16 & 7)
+            *reinterpret_cast<float4*>(slot + (nt ? 0 : 8192) + swb[mt & 1] + 64 * mt + 256 * hf) =
+                make_float4(v[0], v[1], v[2], v[3]);
+          } else {                                  // row o of the 32: 8-B unit (4 mt + g + 16 hf) ^ sg
+            *reinterpret_cast<uint2*>(slot + 8192 + 4096 * nt + swb[mt] + 128 * hf) =
                 make_uint2(pack16<XT>(v[0], v[1]), pack16<XT>(v[2], v[3]));
           }
         }
@@ -523,31 +539,38 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     }
 #endif
     SUBSTAMP(57);
-    // staged rows -> global: each instruction stores 1 KiB = RPI whole y rows of the group
+    // staged rows -> global: each instruction stores 1 KiB = RPI whole y rows of the group. The
+    // y rows of the group start the buffer (rows past nvalid fall outside it and are dropped);
+    // lane offsets are two or four bases plus immediates.
     constexpr int RB = B * ESY, RPI = 1024 / RB, LPR = 64 / RPI;   // row bytes, rows/store, lanes/row
-    const int w = l & (LPR - 1);
+    const int w = l & (LPR - 1), lr = (int)((unsigned)l / LPR);
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (char*)yv + (tok_ok ? tok : 0) * M * ESY + (int64_t)grp_o * NOG * RB, 0,
+        tok_ok ? (int)((M - (int64_t)grp_o * NOG * B) * ESY) : 0, 0x00020000);
+    const int vofs = lr * RB + 16 * w;
+    // LDS read bases: fp32 row s16 = 2 q + lr, unit w ^ (s16 & 7) = (w ^ lr) ^ 2 (q & 3);
+    // 16-bit row rr = 4 q + lr, unit w ^ (rr & 7) = (w ^ lr) ^ 4 (q & 1)
+    int rdb[Y32 ? 4 : 2];
+#pragma unroll
+    for (int c = 0; c < (Y32 ? 4 : 2); ++c)
+      rdb[c] = lr * RB + 16 * ((w ^ lr) ^ (Y32 ? 2 * c : 4 * c));
 #pragma unroll
     for (int half = 0; half < (Y32 ? 2 : 1); ++half) {   // 8 store instructions at a time
       uint4 d[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const int rr = 8 * RPI * half + q * RPI + (int)((unsigned)l / LPR);   // y row of the group
-        if constexpr (Y32) {
-          const int s16 = rr & 15;
-          const char* stg = slot + (rr >= 16 ? 0 : 8192);
-          d[q] = *reinterpret_cast<const uint4*>(stg + 512 * s16 + 16 * (w ^ (s16 & 7)));
+        if constexpr (Y32) {                        // rows 16 half + 2 q + lr: N-tile half's staging
+          d[q] = *reinterpret_cast<const uint4*>(slot + (half ? 0 : 8192) + 1024 * q + rdb[q & 3]);
         } else {
-          uint4 v = *reinterpret_cast<const uint4*>(slot + 8192 + 256 * rr + 16 * (w ^ (rr & 7)));
-          if ((8 * RPI * half + q * RPI) & 8) v = make_uint4(v.z, v.w, v.x, v.y);   // 8-B halves swapped
+          uint4 v = *reinterpret_cast<const uint4*>(slot + 8192 + 1024 * q + rdb[q & 1]);
+          if (q & 2) v = make_uint4(v.z, v.w, v.x, v.y);   // rows with bit 3: 8-B halves swapped
           d[q] = v;
         }
       }
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int rr = 8 * RPI * half + q * RPI + (int)((unsigned)l / LPR);
-        const int yoff = rr < nvalid ? (grp_o * NOG + rr) * RB + 16 * w : 0x7fff0000;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs, yoff, 0, 0);
-      }
+      for (int q = 0; q < 8; ++q)                   // byte offset of row 8 RPI half + RPI q + lr
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs,
+                                               vofs + (8 * half + q) * 1024, 0, 0);
     }
     SUBSTAMP(58);
   };
@@ -615,7 +638,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
 }  // namespace bcfft
 
 namespace {
-template <int XT, bool YF32, bool YSP>
+template <int XT, bool YF32, bool EX>
 void launch_dm(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt, void* y,
                hipStream_t s) {
   const int groups = (n_out + 31) / 32;
@@ -625,7 +648,7 @@ void launch_dm(const void* x, int64_t n, int n_out, const void* spec, const void
   if (total > groups * n_mtiles) total = groups * n_mtiles;
   if (total < groups) total = groups;
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
-  hipLaunchKernelGGL((bcfft::bc_forward_dm_kernel<XT, YF32, YSP>), dim3((unsigned)total), dim3(512), 0, s, x, n,
+  hipLaunchKernelGGL((bcfft::bc_forward_dm_kernel<XT, YF32, EX>), dim3((unsigned)total), dim3(512), 0, s, x, n,
                      n_out, stat, bias, bias_dt, y);
 }
 }  // namespace

@@ -7,11 +7,12 @@ are checked on the CPU against the oracle before the GPU runs them:
 
   stage 1  per (token, half h of 16 input blocks): s = 2^sx with 2^sx * 2 max|x| < 2^15;
            a_t = (x_t + x_{t+64}) s, d_t = (x_t - x_{t+64}) s (t < 64), each split into fp16
-           hi (round toward zero) + lo; X = [a Fe | d Fo] with the fp16 table F = DFT * 2^-7
-           (fp32 accumulation), i.e. X * 2^(sx - 7); split again into fp16 hi + lo.
+           hi (round toward zero) + lo (exact) or rounded once to fp16 (RNE); X = [a Fe | d Fo]
+           with the fp16 table F = DFT * 2^-7 (fp32 accumulation), i.e. X * 2^(sx - 7); split
+           into fp16 hi + lo.
   stage 2  per packed bin: the halves brought to the token's smaller exponent (exact), times the
            STAT image conj(C)/(2b) s_C (fp16), bin 0 with an extra 1/2; Y * 2^-21 split into fp16
-           hi + lo (ysplit, the product build) or rounded once to fp16.
+           hi + lo (exact) or rounded once to fp16.
   stage 3  E = Fe Y16_even, O = Fo Y16_odd (fp32 accumulation); y_t = (E + O) sc,
            y_{t+64} = (E - O) sc with sc = 2^(30 - nmin) / s_C.
 """
@@ -69,8 +70,13 @@ def stat_image(c):
     return re, im, 1.0 / sc                                  # im of bins > 0 are Im(C) (not conj)
 
 
-def dm_forward(x, c, ysplit=True):
-    """x (N, K) float32, c (nO, nI, 128): the kernel's fp32 output (no bias)."""
+def _rne16(v):
+    return np.asarray(v, np.float32).astype(np.float16).astype(np.float64)
+
+
+def dm_forward(x, c, exact=True):
+    """x (N, K) float32, c (nO, nI, 128): the kernel's fp32 output (no bias). exact: the
+    BCFFT_ALGO_DFTX variant (a, d and Y as hi + lo); else "dft" (one RNE term each)."""
     n, k = x.shape
     no, ni, b = c.shape
     assert b == 128 and ni * b == k and ni % 16 == 0
@@ -91,10 +97,14 @@ def dm_forward(x, c, ysplit=True):
             lo, hi = blk[:, :64], blk[:, 64:]
             a = ((lo + hi).astype(np.float32) * np.float32(s)).astype(np.float64)
             d = ((lo - hi).astype(np.float32) * np.float32(s)).astype(np.float64)
-            ah, al = _split16(a)
-            dh, dl = _split16(d)
-            ev = (ah @ Fe + al @ Fe).astype(np.float32)          # (16, 64): even packed bins
-            od = (dh @ Fo + dl @ Fo).astype(np.float32)
+            if exact:
+                ah, al = _split16(a)
+                dh, dl = _split16(d)
+                ev = (ah @ Fe + al @ Fe).astype(np.float32)      # (16, 64): even packed bins
+                od = (dh @ Fo + dl @ Fo).astype(np.float32)
+            else:
+                ev = (_rne16(a) @ Fe).astype(np.float32)
+                od = (_rne16(d) @ Fo).astype(np.float32)
             # packed bins: even f = 2j at ev[:, 2j], ev[:, 2j+1]; odd f = 2j+1 at od[:, 2j], od[:, 2j+1]
             pk = np.zeros((16, 64, 2))
             pk[:, 0::2, 0], pk[:, 0::2, 1] = ev[:, 0::2], ev[:, 1::2]
@@ -114,11 +124,11 @@ def dm_forward(x, c, ysplit=True):
         Y[:, 1:, 0], Y[:, 1:, 1] = yr, yi
         Y[:, 0, 0], Y[:, 0, 1] = y0, y64
         ys = (Y.astype(np.float32) * np.float32(2.0 ** -21)).astype(np.float32)
-        if ysplit:
+        if exact:
             yh, yl = _split16(ys)
             Y16 = yh + yl
         else:
-            Y16 = ys.astype(np.float16).astype(np.float64)
+            Y16 = _rne16(ys)
         # stage 3: columns in table order
         ye = np.stack([Y16[:, 0::2, 0], Y16[:, 0::2, 1]], -1).reshape(no, 64)
         yo = np.stack([Y16[:, 1::2, 0], Y16[:, 1::2, 1]], -1).reshape(no, 64)

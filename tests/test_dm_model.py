@@ -17,17 +17,17 @@ def test_table_matches_dft():
     assert np.allclose(F[:, 64 + 2 * 5 + 1], -np.sin(2 * np.pi * 11 * t / 128), atol=1e-3)
 
 
-@pytest.mark.parametrize("scale,ysplit", [(1.0, True), (1e-5, True), (3e4, True), (1.0, False), (1e-5, False), (3e4, False)])
-def test_dm_model_vs_oracle(scale, ysplit):
+@pytest.mark.parametrize("scale,exact", [(1.0, True), (1e-5, True), (3e4, True), (1.0, False), (1e-5, False), (3e4, False)])
+def test_dm_model_vs_oracle(scale, exact):
     rng = np.random.default_rng(7)
     x = (rng.standard_normal((6, 4096)) * scale).astype(np.float32)
     x[1] *= 1e3                                    # token scales differ
     x[2, 100] = 500 * scale                        # one big channel in half 0
     c = (rng.standard_normal((32, 32, 128)) * 0.01).astype(np.float32)
     ref = orc.bc_forward(x, c)
-    got = dm_forward(x, c, ysplit)
+    got = dm_forward(x, c, exact)
     rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
-    assert rel < (3.2e-4 if ysplit else 4e-4), rel
+    assert rel < (3.2e-4 if exact else 4.8e-4), rel
     for t in range(x.shape[0]):                   # per token as well
         r = np.linalg.norm(got[t] - ref[t]) / np.linalg.norm(ref[t])
         assert r < 6e-4, (t, r)
