@@ -88,6 +88,12 @@ __device__ __forceinline__ void split2(float a, float b, uint32_t& hi, uint32_t&
   hi = pk_rtz(a, b);
   lo = pk_rtz(sub_lo16(a, hi), sub_hi16(b, hi));
 }
+// max(m, |a|, |b|) in one v_max3_f32 (hipcc canonicalises |a| through an extra v_max first)
+__device__ __forceinline__ float amax3(float m, float a, float b) {
+  float r;
+  asm("v_max3_f32 %0, |%1|, |%2|, %3" : "=v"(r) : "v"(a), "v"(b), "v"(m));
+  return r;
+}
 // max |v| over the wave as an integer max of the magnitude bits (no NaN canonicalisation)
 __device__ __forceinline__ uint32_t wave_umax(uint32_t v) {
   v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true));   // quad xor 1
@@ -140,6 +146,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
   // n_tokens). LDS is lane-linear per piece, so the slot's unit swizzle (logical 16-B unit u of
   // block row r at physical u ^ (r & 15)) is applied to the global source offsets.
   auto dma_token = [&](int64_t m, char* region, int q0, int q1) {   // pieces [q0, q1)
+#ifdef BCFFT_DM_NOMEM                               // analysis build: compute only (no x, no y)
+    return;
+#endif
     const int64_t tok = m * TT + tslot;
     const bool ok = tok < n_tokens;
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
@@ -264,13 +273,17 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
           }
         }
       SUBSTAMP(55 + 4 * hh);
-      float mxf = 0.f;                              // max |x| (v_max3_f32 with |.| modifiers)
+      float m0 = 0.f, m1 = 0.f;                     // max |x|: two v_max3_f32 chains
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int pt = 0; pt < 2; ++pt)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) mxf = __builtin_fmaxf(mxf, __builtin_fabsf(xv8[ks][pt][j]));
+          for (int j = 0; j < 8; j += 4) {
+            m0 = amax3(m0, xv8[ks][pt][j], xv8[ks][pt][j + 1]);
+            m1 = amax3(m1, xv8[ks][pt][j + 2], xv8[ks][pt][j + 3]);
+          }
+      const float mxf = __builtin_fmaxf(m0, m1);
       // across lanes as magnitude bits: no NaN canonicalisation around the DPP moves
       const int sx = stat_scale_exp(2.f * __uint_as_float(wave_umax(__float_as_uint(mxf))));   // |a|, |d| <= 2 max|x|
       if (l == 0) wsc[par * 8 + wave * 2 + h] = sx - 7;     // X = D 2^-(sx - 7): the table's 2^-7
@@ -567,6 +580,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
           d[q] = v;
         }
       }
+#ifdef BCFFT_DM_NOMEM
+      if (tok < 0)                                  // never (analysis build): keeps the staging reads
+#endif
 #pragma unroll
       for (int q = 0; q < 8; ++q)                   // byte offset of row 8 RPI half + RPI q + lr
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs,

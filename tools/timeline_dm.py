@@ -11,7 +11,8 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["BCFFT_LIB_PATH"] = os.path.join(ROOT, "llama-fft_amd", "lib", "libbcfft_stamps.so")
+os.environ["BCFFT_LIB_PATH"] = os.path.join(ROOT, "llama-fft_amd", "lib",
+                                           os.environ.get("TIMELINE_LIB", "libbcfft_stamps.so"))
 sys.path.insert(0, os.path.join(ROOT, "llama-fft_amd"))
 import torch  # noqa: E402
 from bcfft import _lib, ops  # noqa: E402
@@ -66,7 +67,7 @@ def run(m, io, n, k=4096, b=128):
         print(f"wave {w}    " + " ".join(f"{v:10.0f}" for v in med))
     if tiles > 4:                                # sub-phases of iteration 4 (from its loop top)
         top = st[:, 1 + 6 * 4]
-        fsub = ["x read h0", "scale h0", "mfma h0", "X wr h0", "x read h1", "scale h1", "mfma h1", "X wr h1"]
+        fsub = ["dma wait", "h0 rd+max", "h0 mfma", "h0 X wr", "h1 rd+max", "h1 mfma", "h1 X wr", "-"]
         isub = ["Y+G read", "-", "compute", "stores", "-", "-", "-", "-"]
         for name, sel, lab in (("F", wv < 4, fsub), ("I", wv >= 4, isub)):
             prev = top[sel]
