@@ -151,11 +151,13 @@ def time_glu(dev, steps, k=4096, m=11008, b=128, n=8192, io="bf16"):
         return s.elapsed_time(e) / steps
 
     with torch.inference_mode():
-        fused = run(lambda: ops.forward_glu(x, sgu, b, m))
+        fused = run(lambda: ops.forward_glu(x, sgu, b, m, algo="auto"))
+        fused_stat = run(lambda: ops.forward_glu(x, sgu, b, m, algo="stationary"))
         unfused = run(lambda: torch.nn.functional.silu(ops.forward(x, sg, None, b, m)) * ops.forward(x, su, None, b, m))
     nbytes = n * k * SZ[io] + n * m * SZ[io] + 2 * (m // b) * (k // b) * (b // 2 + 1) * 8
-    return {"workload": f"gate/up {k}->{m} b={b} N={n} {io}-io + SwiGLU", "engine": "stationary-glu",
-            "ms": round(fused, 4), "unfused_ms": round(unfused, 4),
+    engine = "dft-glu" if resolved_kernel("auto", k, b)[0] == "dft" else "stationary-glu"
+    return {"workload": f"gate/up {k}->{m} b={b} N={n} {io}-io + SwiGLU", "engine": engine,
+            "ms": round(fused, 4), "stationary_glu_ms": round(fused_stat, 4), "unfused_ms": round(unfused, 4),
             "GB_s": round(nbytes / (fused * 1e-3) / 1e9, 1),
             "frac": round(nbytes / (fused * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 

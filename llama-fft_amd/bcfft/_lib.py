@@ -47,6 +47,9 @@ _SIGNATURES = {
     "bcfft_forward_glu": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p]),
+    "bcfft_forward_glu_algo": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_int, ctypes.c_void_p]),
     "bcfft_project_circulant": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "bcfft_grad_c_workspace_bytes": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int]),

@@ -69,9 +69,14 @@ def glu_weights(c_gate: torch.Tensor, c_up: torch.Tensor) -> torch.Tensor:
     return flat.reshape(groups * 32, n_in, b)
 
 
-def forward_glu(x2d: torch.Tensor, spec_gu: torch.Tensor, block_size: int, gate_features: int) -> torch.Tensor:
-    """h = silu(BC_gate(x2d)) * BC_up(x2d) in one launch (bcfft_forward_glu); spec_gu =
-    spectra(glu_weights(c_gate, c_up)). h has x2d's dtype."""
+def forward_glu(x2d: torch.Tensor, spec_gu: torch.Tensor, block_size: int, gate_features: int,
+                algo: str | None = None) -> torch.Tensor:
+    """h = silu(BC_gate(x2d)) * BC_up(x2d) in one launch (bcfft_forward_glu_algo); spec_gu =
+    spectra(glu_weights(c_gate, c_up)). h has x2d's dtype. algo: None -> BCFFT_ALGO env (auto:
+    the DFT kernel at b = 128 with K = 4096, else stationary), or "stationary" / "dft" / "dftx"."""
+    algo = default_algo() if algo is None else algo
+    if algo not in ("auto", "stationary", "dft", "dftx"):
+        algo = "auto"                               # mfma / valu have no fused gate/up form
     _lib.require_device(x2d, "bcfft.forward_glu")
     n, k = x2d.shape
     if block_size > 0 and gate_features % block_size == 0 and k % block_size == 0:
@@ -84,9 +89,9 @@ def forward_glu(x2d: torch.Tensor, spec_gu: torch.Tensor, block_size: int, gate_
     if n == 0:
         return h
     lib = _lib.load()
-    _lib.check(lib.bcfft_forward_glu(x2d.data_ptr(), _lib.dtype_code(x2d.dtype), n, k, gate_features,
-                                     block_size, spec_gu.data_ptr(), h.data_ptr(),
-                                     _lib.stream_handle(x2d.device)), "bcfft_forward_glu")
+    _lib.check(lib.bcfft_forward_glu_algo(x2d.data_ptr(), _lib.dtype_code(x2d.dtype), n, k, gate_features,
+                                          block_size, spec_gu.data_ptr(), h.data_ptr(), _lib.ALGOS[algo],
+                                          _lib.stream_handle(x2d.device)), "bcfft_forward_glu")
     return h
 
 

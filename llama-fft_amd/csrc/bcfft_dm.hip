@@ -109,7 +109,7 @@ __device__ __forceinline__ f16x8 frag(uint32_t a, uint32_t b, uint32_t c, uint32
 }
 }  // namespace dmk
 
-template <int XT, bool YF32, bool EX>
+template <int XT, bool YF32, bool EX, bool GLU>
 __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_out, const uint32_t* __restrict__ stat,
     const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
@@ -134,7 +134,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool fwave = wave < 4;                      // F waves: stage 1 of token slot `wave`
   const int tslot = wave & 3;                       // I waves: stage 3 of token slot wave - 4
-  const int n_groups = (n_out + NOG - 1) / NOG;
+  // GLU (fused gate/up + SwiGLU): n_out counts h blocks; group g holds gate blocks [16g, 16g+16)
+  // in N-tile 0 and the matching up blocks in N-tile 1, and stores 16 h rows
+  constexpr int OPG = GLU ? NOG / 2 : NOG;          // output blocks stored per group
+  const int n_groups = (n_out + OPG - 1) / OPG;
   const int grp_o = blockIdx.x % n_groups;
   const int wg_in_grp = blockIdx.x / n_groups;
   const int64_t M = (int64_t)n_out * B;
@@ -475,7 +478,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     SUBSTAMP(56);
     const int64_t tok = mp * TT + tslot;
     const bool tok_ok = tok < n_tokens;
-    const int nvalid = n_out - grp_o * NOG;
+    const int nvalid = n_out - grp_o * OPG;
     // staging write bases (lane part of the XOR-swizzled address; the rest are immediates).
     // fp32: (4 mt + g) ^ s = 4 mt + (g ^ (s & 3)) +- 4 (s >> 2) by the parity of mt (s = o16 & 7);
     // 16-bit: (4 mt + g) ^ sg for each mt (sg = ((o16 & 7) << 1) | (o16 >> 3))
@@ -510,6 +513,30 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
             O[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][1], __builtin_bit_cast(f16x8, yf[yp][ks][1][nt]), O[nt], 0, 0, 0);
           }
       // rows t = 16 mt + 4 g + r (and t + 64), column o = 16 nt + o16
+      if constexpr (GLU) {                          // h = silu(gate) * up of block o16
+        float gu[NT][2][4];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)             // gate / up rounded to x's dtype (:266)
+              gu[nt][hf][r] = round_to(hf ? fmaf(E[nt][r], ysc, -O[nt][r] * ysc) : fmaf(E[nt][r], ysc, O[nt][r] * ysc), XT);
+        }
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)               // torch: silu rounded, then the product rounded
+            v[r] = round_to(round_to(silu(gu[0][hf][r]), XT) * gu[1][hf][r], XT);
+          if constexpr (Y32) {
+            *reinterpret_cast<float4*>(slot + 8192 + swb[mt & 1] + 64 * mt + 256 * hf) = make_float4(v[0], v[1], v[2], v[3]);
+          } else {
+            *reinterpret_cast<uint2*>(slot + 8192 + swb[mt] + 128 * hf) =
+                make_uint2(pack16<XT>(v[0], v[1]), pack16<XT>(v[2], v[3]));
+          }
+        }
+      } else
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const int o = 16 * nt + o16;
@@ -558,8 +585,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     constexpr int RB = B * ESY, RPI = 1024 / RB, LPR = 64 / RPI;   // row bytes, rows/store, lanes/row
     const int w = l & (LPR - 1), lr = (int)((unsigned)l / LPR);
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
-        (char*)yv + (tok_ok ? tok : 0) * M * ESY + (int64_t)grp_o * NOG * RB, 0,
-        tok_ok ? (int)((M - (int64_t)grp_o * NOG * B) * ESY) : 0, 0x00020000);
+        (char*)yv + (tok_ok ? tok : 0) * M * ESY + (int64_t)grp_o * OPG * RB, 0,
+        tok_ok ? (int)((M - (int64_t)grp_o * OPG * B) * ESY) : 0, 0x00020000);
+    constexpr int NQ = GLU && !Y32 ? 4 : 8;         // store instructions per half (GLU 16-bit: 16 rows)
     const int vofs = lr * RB + 16 * w;
     // LDS read bases: fp32 row s16 = 2 q + lr, unit w ^ (s16 & 7) = (w ^ lr) ^ 2 (q & 3);
     // 16-bit row rr = 4 q + lr, unit w ^ (rr & 7) = (w ^ lr) ^ 4 (q & 1)
@@ -568,10 +596,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     for (int c = 0; c < (Y32 ? 4 : 2); ++c)
       rdb[c] = lr * RB + 16 * ((w ^ lr) ^ (Y32 ? 2 * c : 4 * c));
 #pragma unroll
-    for (int half = 0; half < (Y32 ? 2 : 1); ++half) {   // 8 store instructions at a time
+    for (int half = 0; half < (Y32 && !GLU ? 2 : 1); ++half) {   // 8 store instructions at a time
       uint4 d[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
+      for (int q = 0; q < NQ; ++q) {
         if constexpr (Y32) {                        // rows 16 half + 2 q + lr: N-tile half's staging
           d[q] = *reinterpret_cast<const uint4*>(slot + (half ? 0 : 8192) + 1024 * q + rdb[q & 3]);
         } else {
@@ -584,7 +612,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
       if (tok < 0)                                  // never (analysis build): keeps the staging reads
 #endif
 #pragma unroll
-      for (int q = 0; q < 8; ++q)                   // byte offset of row 8 RPI half + RPI q + lr
+      for (int q = 0; q < NQ; ++q)                  // byte offset of row 8 RPI half + RPI q + lr
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs,
                                                vofs + (8 * half + q) * 1024, 0, 0);
     }
@@ -654,18 +682,18 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
 }  // namespace bcfft
 
 namespace {
-template <int XT, bool YF32, bool EX>
+template <int XT, bool YF32, bool EX, bool GLU = false>
 void launch_dm(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt, void* y,
                hipStream_t s) {
-  const int groups = (n_out + 31) / 32;
-  const bcfft::SpecLayout sl = bcfft::spec_layout(n_out, 32, 128);
+  const int groups = GLU ? (n_out + 15) / 16 : (n_out + 31) / 32;
+  const bcfft::SpecLayout sl = bcfft::spec_layout(GLU ? 32 * groups : n_out, 32, 128);
   const int64_t n_mtiles = (n + 3) / 4;
   int64_t total = bcfft::device_cu_count();
   if (total > groups * n_mtiles) total = groups * n_mtiles;
   if (total < groups) total = groups;
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
-  hipLaunchKernelGGL((bcfft::bc_forward_dm_kernel<XT, YF32, EX>), dim3((unsigned)total), dim3(512), 0, s, x, n,
-                     n_out, stat, bias, bias_dt, y);
+  hipLaunchKernelGGL((bcfft::bc_forward_dm_kernel<XT, YF32, EX, GLU>), dim3((unsigned)total), dim3(512), 0, s, x,
+                     n, n_out, stat, bias, bias_dt, y);
 }
 }  // namespace
 
@@ -697,6 +725,22 @@ bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, bool exact, const vo
   else if (yf32) BCFFT_DM_LAUNCH(BCFFT_BF16, true);
   else BCFFT_DM_LAUNCH(BCFFT_BF16, false);
 #undef BCFFT_DM_LAUNCH
+  return true;
+}
+
+// fused gate/up + SwiGLU (bcfft_forward_glu): h has x's dtype, no bias; fp16 takes the exact variant
+bool launch_forward_dm_glu(int b, int n_in, int xdt, bool exact, const void* x, int64_t n, int n_gate,
+                           const void* spec, void* h, hipStream_t s) {
+  if (!dm_eligible(n_in, b)) return false;
+  if (xdt == BCFFT_F32) {
+    if (exact) launch_dm<BCFFT_F32, true, true, true>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
+    else launch_dm<BCFFT_F32, true, false, true>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
+  } else if (xdt == BCFFT_F16) {
+    launch_dm<BCFFT_F16, false, true, true>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
+  } else {
+    if (exact) launch_dm<BCFFT_BF16, false, true, true>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
+    else launch_dm<BCFFT_BF16, false, false, true>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
+  }
   return true;
 }
 }  // namespace bcfft

@@ -811,8 +811,10 @@ int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_feat
                           bias_dtype, y, y_dtype, algo, nullptr, 0, stream);
 }
 
-int bcfft_forward_glu(const void* x, int x_dtype, int64_t n_tokens, int in_features, int gate_features,
-                      int block_size, const void* spectra_gu, void* h, void* stream) {
+int bcfft_forward_glu_algo(const void* x, int x_dtype, int64_t n_tokens, int in_features, int gate_features,
+                           int block_size, const void* spectra_gu, void* h, int algo, void* stream) {
+  if (algo != BCFFT_ALGO_AUTO && algo != BCFFT_ALGO_STAT && algo != BCFFT_ALGO_DFT && algo != BCFFT_ALGO_DFTX)
+    return BCFFT_ERR_ARG;
   if (!valid_block(block_size)) return BCFFT_ERR_BLOCK;
   if (n_tokens < 0 || in_features <= 0 || gate_features <= 0 || in_features % block_size ||
       gate_features % block_size)
@@ -820,11 +822,24 @@ int bcfft_forward_glu(const void* x, int x_dtype, int64_t n_tokens, int in_featu
   if (!valid_dt(x_dtype)) return BCFFT_ERR_DTYPE;
   const int n_in = in_features / block_size, n_gate = gate_features / block_size;
   if (!bcfft::stat_eligible(n_in, block_size)) return BCFFT_ERR_BLOCK;
+  const bool dm = bcfft::dm_eligible(n_in, block_size);
+  if (algo == BCFFT_ALGO_AUTO) algo = dm ? BCFFT_ALGO_DFT : BCFFT_ALGO_STAT;
+  if (algo != BCFFT_ALGO_STAT && !dm) return BCFFT_ERR_BLOCK;
   if (n_tokens == 0) return BCFFT_OK;
   if (!x || !h || !spectra_gu) return BCFFT_ERR_ARG;
   if (!aligned16(x) || !aligned16(h) || !aligned16(spectra_gu)) return BCFFT_ERR_ALIGN;
-  bcfft::launch_forward_glu(block_size, n_in, x_dtype, x, n_tokens, n_gate, spectra_gu, h, (hipStream_t)stream);
+  if (algo == BCFFT_ALGO_STAT)
+    bcfft::launch_forward_glu(block_size, n_in, x_dtype, x, n_tokens, n_gate, spectra_gu, h, (hipStream_t)stream);
+  else
+    bcfft::launch_forward_dm_glu(block_size, n_in, x_dtype, algo == BCFFT_ALGO_DFTX, x, n_tokens, n_gate, spectra_gu,
+                                 h, (hipStream_t)stream);
   return record_launch();
+}
+
+int bcfft_forward_glu(const void* x, int x_dtype, int64_t n_tokens, int in_features, int gate_features,
+                      int block_size, const void* spectra_gu, void* h, void* stream) {
+  return bcfft_forward_glu_algo(x, x_dtype, n_tokens, in_features, gate_features, block_size, spectra_gu, h,
+                                BCFFT_ALGO_AUTO, stream);
 }
 
 int bcfft_forward(const void* x, int x_dtype, int64_t n_tokens, int in_features,

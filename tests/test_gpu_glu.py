@@ -4,8 +4,8 @@ patch_mlp_with_block_circulant's gate/up projections (patch_llama_fft.py:343-394
 
 The oracle follows torch on the reference's tensors: gate(x) and up(x) rounded to x's dtype
 (the BC forward's .to(x.dtype), patch_llama_fft.py:266), SiLU computed in fp32 and rounded,
-the product rounded. The weights are the stationary kernel's fp16 (~3e-4 per output), and SiLU
-and the product carry that error along, so fp32 outputs are checked at 1e-3 relative Frobenius
+the product rounded. The weights are fp16 in both engines (stationary ~3e-4 per output, DFT
+~4e-4, `dftx` ~3e-4), and SiLU and the product carry that error along, so fp32 outputs are checked at 1e-3 relative Frobenius
 and 16-bit outputs within ~2 output ulp plus 2e-3 (the weight error SiLU can amplify) per
 element, plus the norm bound."""
 import numpy as np
@@ -50,10 +50,13 @@ def _check(h, ref, xdt):
     else:
         ulp = 2.0 ** -7 if xdt == "bfloat16" else 2.0 ** -10
         rms = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
-        # 2 output ulp of rounding plus the weights' ~3e-4 carried through SiLU, whose relative
-        # sensitivity |1 + g (1 - sigmoid(g))| reaches ~|g| for negative g: 2e-3 per element
-        bad = np.abs(g - ref) > (2 * ulp + 2e-3) * np.abs(ref) + 2 * ulp * rms
-        assert not bad.any(), f"{int(bad.sum())} elements beyond ~2 ulp"
+        # 2 output ulp of rounding plus the weights' ~3-4e-4 carried through SiLU, whose relative
+        # sensitivity |1 + g (1 - sigmoid(g))| reaches ~|g| for negative g: 2e-3 per element, and
+        # an absolute 4 ulp of the rms (the weight error of large |u| * |g| products: measured
+        # worst 3.1 with the DFT engine, fp16, 262k elements)
+        bad = np.abs(g - ref) > (2 * ulp + 2e-3) * np.abs(ref) + 4 * ulp * rms
+        worst = float(np.max(np.abs(g - ref) / ((2 * ulp + 2e-3) * np.abs(ref) + ulp * rms)))
+        assert not bad.any(), f"{int(bad.sum())} elements beyond ~2 ulp (worst {worst:.2f} ulp of rms)"
         assert e < 4e-3, e
     return e
 
@@ -69,31 +72,36 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("algo", ["auto", "stationary", "dftx"])
 @pytest.mark.parametrize("k,m,b,n,xdt", CASES)
-def test_glu_vs_oracle(dev, k, m, b, n, xdt):
+def test_glu_vs_oracle(dev, k, m, b, n, xdt, algo):
+    if b != 128 and algo == "dftx":
+        pytest.skip("the DFT kernel serves b = 128 with K = 4096")
     from bcfft import ops
     rng = np.random.default_rng(k + m + b + n)
     cg = (rng.standard_normal((m // b, k // b, b)) * 0.01).astype(np.float32)
     cu = (rng.standard_normal((m // b, k // b, b)) * 0.01).astype(np.float32)
     x = rng.standard_normal((n, k)).astype(np.float32)
     spec = ops.spectra(ops.glu_weights(torch.from_numpy(cg).to(dev), torch.from_numpy(cu).to(dev)))
-    h = ops.forward_glu(torch.from_numpy(x).to(dev).to(TDT[xdt]), spec, b, m)
+    h = ops.forward_glu(torch.from_numpy(x).to(dev).to(TDT[xdt]), spec, b, m, algo=algo)
     torch.cuda.synchronize()
     assert h.dtype == TDT[xdt] and h.shape == (n, m)
     _check(h, oracle_glu(x, cg, cu, xdt), xdt)
 
 
-def test_glu_equals_unfused_composition(dev):
-    """The fused launch against the two stationary launches + torch SiLU and product."""
+@pytest.mark.parametrize("algo", ["stationary", "dft"])
+def test_glu_equals_unfused_composition(dev, algo):
+    """The fused launch against the same engine's two separate launches + torch SiLU and product
+    (the fused weights share one fp16 scale, so roundings differ slightly)."""
     from bcfft import ops
     torch.manual_seed(3)
     k, m, b = 4096, 11008, 128
     cg = torch.randn(m // b, k // b, b, device=dev) * 0.01
     cu = torch.randn(m // b, k // b, b, device=dev) * 0.01
     x = torch.randn(301, k, device=dev).to(torch.bfloat16)
-    h = ops.forward_glu(x, ops.spectra(ops.glu_weights(cg, cu)), b, m)
-    ref = (torch.nn.functional.silu(ops.forward(x, ops.spectra(cg), None, b, m, algo="stationary"))
-           * ops.forward(x, ops.spectra(cu), None, b, m, algo="stationary"))
+    h = ops.forward_glu(x, ops.spectra(ops.glu_weights(cg, cu)), b, m, algo=algo)
+    ref = (torch.nn.functional.silu(ops.forward(x, ops.spectra(cg), None, b, m, algo=algo))
+           * ops.forward(x, ops.spectra(cu), None, b, m, algo=algo))
     d = (h.float() - ref.float()).abs()
     assert (d <= 2 * 2.0 ** -7 * ref.float().abs() + 1e-6).float().mean().item() > 0.999
     assert ((h.float() - ref.float()).norm() / ref.float().norm()).item() < 4e-3
@@ -105,6 +113,10 @@ def test_glu_rejects_ineligible_geometry(dev):
     spec = ops.spectra(ops.glu_weights(cg, cg))
     with pytest.raises(RuntimeError, match="block_size"):
         ops.forward_glu(torch.zeros(3, 512, device=dev), spec, 128, 512)
+    c64 = torch.zeros(8, 32, 64, device=dev)                  # stationary geometry, not the DFT one
+    spec64 = ops.spectra(ops.glu_weights(c64, c64))
+    with pytest.raises(RuntimeError, match="block_size"):
+        ops.forward_glu(torch.zeros(3, 2048, device=dev), spec64, 64, 512, algo="dft")
 
 
 def test_fused_mlp_module_matches_unfused(dev):
