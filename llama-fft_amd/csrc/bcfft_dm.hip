@@ -29,16 +29,13 @@
 // LDS access pattern is checked conflict-free by tools/lds_banks_dm.py.
 #include "bcfft_device.h"
 #include "bcfft_dm_table.h"
+#include "bcfft_dm_common.h"
 
 
 namespace bcfft {
 
 namespace dmk {
-typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
-typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
-typedef __attribute__((ext_vector_type(4))) short s16x4;
-typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
-typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+using namespace dmh;
 
 constexpr int B = 128, NI = 32, KS = 2, NOG = 32, TT = 4, NW = 8;
 constexpr int BW = 8, NT = 2;                       // bins per wave, 16-wide N-tiles per group
@@ -50,9 +47,6 @@ constexpr int SC_OFF = F_OFF + 16384;               // scale exponents [2 parity
 constexpr int LDS_BYTES = SC_OFF + 64;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 
-// F image: row t, 16-B chunk ch stored at chunk ch ^ fsw(t) (conflict-free for the stage-3 row
-// reads and the stage-1 transposed reads)
-__device__ __forceinline__ int fsw(int t) { return ((t & 3) << 1) | (t & 8); }
 // X unit (16 B = 4 input blocks x (re, im) fp16 of bin f, precision p, block quad q) of the
 // token in slot tok, K-step ks; swizzle: the precision bit flips with bin bit 2, the quad with
 // the token pair
@@ -63,50 +57,6 @@ __device__ __forceinline__ int xunit(int ks, int f, int p, int q, int tok) {
 // the K-step-0 X units of wave w's bins in the same token slot
 __device__ __forceinline__ int yunit(int w, int o, int par) { return w * 1024 + 16 * (32 * par + o); }
 
-__device__ __forceinline__ uint32_t pk_rtz(float a, float b) {
-  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b));
-}
-__device__ __forceinline__ uint32_t pk_rne(float a, float b) {
-  const f16x2 h = {(_Float16)a, (_Float16)b};
-  return __builtin_bit_cast(uint32_t, h);
-}
-__device__ __forceinline__ float lo16(uint32_t p) { return (float)__builtin_bit_cast(f16x2, p).x; }
-__device__ __forceinline__ float hi16(uint32_t p) { return (float)__builtin_bit_cast(f16x2, p).y; }
-// a - f32(fp16 half of h): one v_fma_mix_f32 (hipcc emits a conversion and a subtraction)
-__device__ __forceinline__ float sub_lo16(float a, uint32_t h) {
-  float r;
-  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(r) : "v"(a), "v"(h));
-  return r;
-}
-__device__ __forceinline__ float sub_hi16(float a, uint32_t h) {
-  float r;
-  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(r) : "v"(a), "v"(h));
-  return r;
-}
-// (a, b) -> fp16 hi (toward zero) and lo = the rest (toward zero)
-__device__ __forceinline__ void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
-  hi = pk_rtz(a, b);
-  lo = pk_rtz(sub_lo16(a, hi), sub_hi16(b, hi));
-}
-// max(m, |a|, |b|) in one v_max3_f32 (hipcc canonicalises |a| through an extra v_max first)
-__device__ __forceinline__ float amax3(float m, float a, float b) {
-  float r;
-  asm("v_max3_f32 %0, |%1|, |%2|, %3" : "=v"(r) : "v"(a), "v"(b), "v"(m));
-  return r;
-}
-// max |v| over the wave as an integer max of the magnitude bits (no NaN canonicalisation)
-__device__ __forceinline__ uint32_t wave_umax(uint32_t v) {
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true));   // quad xor 1
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true));   // quad xor 2
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, true));  // row half mirror
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, true));  // row mirror
-  const uint32_t a = max((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16));
-  const uint32_t b = max((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48));
-  return max(a, b);
-}
-__device__ __forceinline__ f16x8 frag(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-  return __builtin_bit_cast(f16x8, make_uint4(a, b, c, d));
-}
 }  // namespace dmk
 
 template <int XT, bool YF32, bool EX, bool GLU>
@@ -719,6 +669,12 @@ bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, bool exact, const vo
 #define BCFFT_DM_LAUNCH(XT, YF)                                                      \
   (exact ? launch_dm<XT, YF, true>(x, n, n_out, spec, bias, bias_dt, y, s)          \
          : launch_dm<XT, YF, false>(x, n, n_out, spec, bias, bias_dt, y, s))
+#ifndef BCFFT_NO_DM8
+  if (!exact && dm8_eligible(n_in, b, xdt, yf32)) {  // bf16 I/O: 8 tokens per tile (bcfft_dm8.hip)
+    launch_forward_dm8(x, n, n_out, spec, bias, bias_dt, y, false, s);
+    return true;
+  }
+#endif
   if (xdt == BCFFT_F32) BCFFT_DM_LAUNCH(BCFFT_F32, true);
   else if (xdt == BCFFT_F16 && yf32) BCFFT_DM_LAUNCH(BCFFT_F16, true);
   else if (xdt == BCFFT_F16) launch_dm<BCFFT_F16, false, true>(x, n, n_out, spec, bias, bias_dt, y, s);
@@ -739,7 +695,11 @@ bool launch_forward_dm_glu(int b, int n_in, int xdt, bool exact, const void* x, 
     launch_dm<BCFFT_F16, false, true, true>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
   } else {
     if (exact) launch_dm<BCFFT_BF16, false, true, true>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
+#ifndef BCFFT_NO_DM8
+    else launch_forward_dm8(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, true, s);   // 8 tokens per tile
+#else
     else launch_dm<BCFFT_BF16, false, false, true>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
+#endif
   }
   return true;
 }

@@ -74,9 +74,10 @@ def _rne16(v):
     return np.asarray(v, np.float32).astype(np.float16).astype(np.float64)
 
 
-def dm_forward(x, c, exact=True):
+def dm_forward(x, c, exact=True, single_x=False):
     """x (N, K) float32, c (nO, nI, 128): the kernel's fp32 output (no bias). exact: the
-    BCFFT_ALGO_DFTX variant (a, d and Y as hi + lo); else "dft" (one RNE term each)."""
+    BCFFT_ALGO_DFTX variant (a, d and Y as hi + lo); else "dft" (one RNE term each). single_x:
+    the bf16-I/O kernel of bcfft_dm8.hip, whose X is one RNE fp16 term too."""
     n, k = x.shape
     no, ni, b = c.shape
     assert b == 128 and ni * b == k and ni % 16 == 0
@@ -109,7 +110,10 @@ def dm_forward(x, c, exact=True):
             pk = np.zeros((16, 64, 2))
             pk[:, 0::2, 0], pk[:, 0::2, 1] = ev[:, 0::2], ev[:, 1::2]
             pk[:, 1::2, 0], pk[:, 1::2, 1] = od[:, 0::2], od[:, 1::2]
-            shi, slo = _split16(pk)
+            if single_x:
+                shi, slo = _rne16(pk), np.zeros_like(pk)
+            else:
+                shi, slo = _split16(pk)
             X[16 * hh:16 * hh + 16] = (shi[..., 0] + slo[..., 0]) + 1j * (shi[..., 1] + slo[..., 1])
             nsc.append(sx - 7)
         nmin = min(nsc)

@@ -31,3 +31,15 @@ def test_dm_model_vs_oracle(scale, exact):
     for t in range(x.shape[0]):                   # per token as well
         r = np.linalg.norm(got[t] - ref[t]) / np.linalg.norm(ref[t])
         assert r < 6e-4, (t, r)
+
+
+def test_dm8_model_single_x_vs_oracle():
+    """The bf16-I/O kernel's arithmetic (X one fp16 term as well) before the bf16 output rounding:
+    well under bf16's own 2^-9."""
+    rng = np.random.default_rng(8)
+    x = rng.standard_normal((4, 4096)).astype(np.float32)
+    c = (rng.standard_normal((32, 32, 128)) * 0.01).astype(np.float32)
+    ref = orc.bc_forward(x, c)
+    got = dm_forward(x, c, exact=False, single_x=True)
+    rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
+    assert rel < 6e-4, rel

@@ -125,3 +125,22 @@ def test_dft_rejects_ineligible_geometry(dev):
     spec = ops.spectra(c)
     with pytest.raises(RuntimeError, match="block_size"):
         ops.forward(torch.zeros(3, 512, device=dev), spec, None, 64, 256, algo="dft")
+
+
+def test_dft8_bf16_matches_numpy_model(dev):
+    """bf16 I/O runs the 8-token kernel (bcfft_dm8.hip: X one fp16 term): its bf16 output equals
+    the numpy mirror's (single_x) rounded to bf16 except for rounding flips at the bf16 ties."""
+    from dm_model import dm_forward
+    rng = np.random.default_rng(12)
+    c = (rng.standard_normal((32, 32, 128)) * 0.01).astype(np.float32)
+    x = rng.standard_normal((21, 4096)).astype(np.float32)   # 3 M-tiles of 8, the last partial
+    x[3] *= 500.0
+    x[9] *= 1e-4
+    xr = O.round_to(x, O.BF16)
+    y, ref = _run(dev, x, c, None, "bfloat16", "bfloat16", algo="dft")
+    g = y.float().cpu().numpy()
+    mdl = O.round_to(dm_forward(xr, O.round_to(c, O.BF16), exact=False, single_x=True), O.BF16)
+    assert np.mean(g == mdl) > 0.97, np.mean(g == mdl)
+    assert rel_err(g, mdl) < 1e-3
+    for t in range(x.shape[0]):
+        assert rel_err(g[t], ref[t]) < 4e-3, t

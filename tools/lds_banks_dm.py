@@ -177,6 +177,66 @@ def staging_roundtrip(es):
     return True
 
 
+def accesses_dm8():
+    """bc_forward_dm8_kernel (bcfft_dm8.hip): 8 token slots of 8,256 B, X one fp16 term"""
+    slot8, region8 = 8192 + 64, 8 * (8192 + 64)
+    f_off = 2 * region8
+
+    def xunit8(ks, f, q):
+        return 4096 * ks + 64 * (f ^ ((f >> 2) & 1)) + 16 * q
+    for reg in (0, 1):
+        rb = reg * region8
+        for w in range(8):
+            slot = rb + w * slot8
+            for h in (0, 1):
+                for ks in (0, 1):
+                    for pt in (0, 1):
+                        yield "dm8 s1 x read", "rd128", [slot + (16 * h + (l & 15)) * 256 + 16 * ((4 * ks + (l >> 4) + 8 * pt) ^ (l & 15))
+                                                         for l in range(64)]
+                for pr in (0, 1):
+                    for mt in range(4):
+                        for bb in (0, 1):
+                            ad = []
+                            for l in range(64):
+                                b16, g = l & 15, l >> 4
+                                a = slot + 4096 * h + 256 * g + 64 * (pr ^ (g & 1)) + 4 * b16 + 1024 * mt + 128 * bb
+                                assert a - slot == xunit8(h, 16 * mt + 4 * g + pr + 2 * bb, b16 >> 2) + 4 * (b16 & 3)
+                                ad.append(a)
+                            yield "dm8 s1 X write", "wr32", ad
+            for fb in range(8):
+                for ks in (0, 1):
+                    ad = []
+                    for l in range(64):
+                        t, kb = (l & 15) >> 1, l >> 4
+                        a = rb + t * slot8 + 512 * w + 16 * kb + 4096 * ks + 64 * (fb ^ ((fb >> 2) & 1))
+                        assert a - rb - t * slot8 == xunit8(ks, 8 * w + fb, kb)
+                        ad.append(a)
+                    yield "dm8 s2 X read", "rd128", ad
+            for s2 in (0, 1):
+                for nt in (0, 1):
+                    for par in (0, 1):
+                        yield "dm8 s2 Y write", "wr128", [rb + (2 * (l >> 4) + s2) * slot8 + 4096 * par + 512 * w + 16 * (16 * nt + (l & 15))
+                                                          for l in range(64)]
+            for ks in (0, 1):
+                for pr in (0, 1):
+                    for nt in (0, 1):
+                        yield "dm8 s3 Y read", "rd128", [slot + 512 * (l >> 4) + 16 * (l & 15) + 4096 * pr + 2048 * ks + 256 * nt
+                                                         for l in range(64)]
+            for mt in range(4):
+                for nt in (0, 1):
+                    for hf in (0, 1):
+                        ad = []
+                        for l in range(64):
+                            o16, g = l & 15, l >> 4
+                            sg = ((o16 & 7) << 1) | (o16 >> 3)
+                            ad.append(slot + 4096 * nt + 256 * o16 + 8 * ((4 * mt + g) ^ sg) + 128 * hf)
+                        yield "dm8 s3 y staging write", "wr64", ad
+            for q in range(8):
+                yield "dm8 s3 y staging read", "rd128", [slot + 1024 * q + (l >> 4) * 256 + 16 * (((l & 15) ^ (l >> 4)) ^ (4 * (q & 1)))
+                                                         for l in range(64)]
+    assert f_off % 256 == 0
+
+
 def main():
     bad = 0
     for es in (4, 2):
@@ -188,6 +248,12 @@ def main():
         for name, c in seen.items():
             print(f"es={es} {name:22s} {'conflict-free' if c == 1 else f'{c}-way'}")
             bad += c > 1
+    seen = {}
+    for name, kind, ad in accesses_dm8():
+        seen[name] = max(seen.get(name, 1), worst(ad, kind))
+    for name, c in seen.items():
+        print(f"bf16 {name:22s} {'conflict-free' if c == 1 else f'{c}-way'}")
+        bad += c > 1
     sys.exit(1 if bad else 0)
 
 
