@@ -45,12 +45,18 @@ def algo_bytes(n, k, m, b, io, bias):
     return n * k * SZ[io] + n * m * SZ[io] + n_out * n_in * (b // 2 + 1) * 8 + (m * SZ[io] if bias else 0)
 
 
-def resolved_kernel(algo, k, b):
-    """(algorithm, kernel symbol, MAC arithmetic) that BCFFT_ALGO=algo runs for this geometry;
-    mirrors bcfft_forward_algo's AUTO rule (csrc/bcfft_kernels.hip)."""
+def resolved_kernel(algo, k, b, io="fp32"):
+    """(algorithm, kernel symbol, MAC arithmetic) that BCFFT_ALGO=algo runs for this geometry and
+    I/O dtype; mirrors bcfft_forward_algo's AUTO rule (csrc/bcfft_kernels.hip)."""
     n_in = k // b
     stat_ok = (b == 128 and n_in == 32) or (b == 64 and n_in in (32, 64))
     dft_ok = b == 128 and n_in == 32
+    if io == "bf16" and algo in ("dft", "auto") and b == 64 and n_in == 64:
+        return ("dft", "bc_forward_dm64_kernel",
+                "MFMA fp16 throughout, b=64, 8 tokens per tile, one-term spectra (bf16 I/O)")
+    if io == "bf16" and algo in ("dft", "auto") and dft_ok:
+        return ("dft", "bc_forward_dm8_kernel",
+                "MFMA fp16 throughout, 8 tokens per tile, one-term spectra (bf16 I/O)")
     if algo == "dftx":
         return ("dftx", "bc_forward_dm_kernel",
                 "MFMA fp16 throughout: block DFT (even/odd split, x hi+lo) x 2^-7 table, stationary "
@@ -261,7 +267,7 @@ def main():
             os.environ["BCFFT_ALGO"] = algo
             vbytes = algo_bytes(vn, vk, vm, vb, vio, False)
             variants.append({"workload": f"{vk}->{vm} b={vb} N={vn} {vio}-io algo={va}",
-                             "engine": resolved_kernel(va, vk, vb)[0],
+                             "engine": resolved_kernel(va, vk, vb, vio)[1].replace("bc_forward_", "").replace("_kernel", ""),
                              "ms": round(vkern, 4),
                              "GTok_elem_s": round(vn * vm / (vkern * 1e-3) / 1e9, 3),
                              "GB_s": round(vbytes / (vkern * 1e-3) / 1e9, 1),
@@ -312,7 +318,7 @@ def main():
 
 
     tag = f"{k}x{m}_b{b}_n{n}_{io}"
-    kname = resolved_kernel(algo, k, b)
+    kname = resolved_kernel(algo, k, b, io if not args.bias else "fp32")
     cpu = None
     if rank == 0 and world == 1 and args.cpu_budget > 0:
         cpu = cpu_baseline(k, m, b, io, bool(args.bias), args.cpu_budget)

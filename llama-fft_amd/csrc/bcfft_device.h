@@ -508,6 +508,9 @@ bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, bool exact, const vo
 bool launch_forward_dm_glu(int b, int n_in, int xdt, bool exact, const void* x, int64_t n, int n_gate,
                            const void* spec, void* h, hipStream_t s);
 bool dm8_eligible(int n_in, int b, int xdt, bool yf32);
+bool dm64_eligible(int n_in, int b, int xdt, bool yf32);
+void launch_forward_dm64(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt,
+                         void* y, bool glu, hipStream_t s);
 void launch_forward_dm8(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt, void* y,
                         bool glu, hipStream_t s);
 

@@ -734,9 +734,9 @@ int bcfft_spectra(const void* c, int c_dtype, int n_out_blocks, int n_in_blocks,
 }
 
 // the algorithm bcfft_forward_algo runs for this geometry (AUTO resolved)
-static int resolve_algo(int algo, int n_in, int block_size) {
+static int resolve_algo(int algo, int n_in, int block_size, int xdt = -1, bool yf32 = true) {
   if (algo != BCFFT_ALGO_AUTO) return algo;
-  if (bcfft::dm_eligible(n_in, block_size)) return BCFFT_ALGO_DFT;
+  if (bcfft::dm_eligible(n_in, block_size) || bcfft::dm64_eligible(n_in, block_size, xdt, yf32)) return BCFFT_ALGO_DFT;
   return bcfft::stat_eligible(n_in, block_size) ? BCFFT_ALGO_STAT
                                                 : (block_size <= 128 ? BCFFT_ALGO_MFMA : BCFFT_ALGO_VALU);
 }
@@ -778,13 +778,18 @@ int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_featur
   const int n_in = in_features / block_size, n_out = out_features / block_size;
   const bool stat_ok = bcfft::stat_eligible(n_in, block_size);
   if (algo == BCFFT_ALGO_STAT && !stat_ok) return BCFFT_ERR_BLOCK;
-  if ((algo == BCFFT_ALGO_DFT || algo == BCFFT_ALGO_DFTX) && !bcfft::dm_eligible(n_in, block_size))
-    return BCFFT_ERR_BLOCK;
-  algo = resolve_algo(algo, n_in, block_size);
+  const bool dm64 = bcfft::dm64_eligible(n_in, block_size, x_dtype, y_dtype == BCFFT_F32);
+  if (algo == BCFFT_ALGO_DFTX && !bcfft::dm_eligible(n_in, block_size)) return BCFFT_ERR_BLOCK;
+  if (algo == BCFFT_ALGO_DFT && !bcfft::dm_eligible(n_in, block_size) && !dm64) return BCFFT_ERR_BLOCK;
+  algo = resolve_algo(algo, n_in, block_size, x_dtype, y_dtype == BCFFT_F32);
   // the workspace is used only when it is as large as bcfft_forward_workspace_bytes asks
   const int64_t need = bcfft_forward_workspace_bytes(n_tokens, in_features, out_features, block_size, algo);
   float* ws = (workspace && need > 0 && workspace_bytes >= need) ? (float*)workspace : nullptr;
   hipStream_t s = (hipStream_t)stream;
+  if (algo == BCFFT_ALGO_DFT && block_size == 64) {
+    bcfft::launch_forward_dm64(x, n_tokens, n_out, spectra, bias, bias_dtype, y, false, s);
+    return record_launch();
+  }
   if (algo == BCFFT_ALGO_DFT || algo == BCFFT_ALGO_DFTX) {
     bcfft::launch_forward_dm(block_size, n_in, x_dtype, y_dtype == BCFFT_F32, algo == BCFFT_ALGO_DFTX, x, n_tokens,
                              n_out, spectra, bias, bias_dtype, y, s);
@@ -823,13 +828,17 @@ int bcfft_forward_glu_algo(const void* x, int x_dtype, int64_t n_tokens, int in_
   const int n_in = in_features / block_size, n_gate = gate_features / block_size;
   if (!bcfft::stat_eligible(n_in, block_size)) return BCFFT_ERR_BLOCK;
   const bool dm = bcfft::dm_eligible(n_in, block_size);
-  if (algo == BCFFT_ALGO_AUTO) algo = dm ? BCFFT_ALGO_DFT : BCFFT_ALGO_STAT;
-  if (algo != BCFFT_ALGO_STAT && !dm) return BCFFT_ERR_BLOCK;
+  const bool dm64 = bcfft::dm64_eligible(n_in, block_size, x_dtype, false);   // h has x's dtype
+  if (algo == BCFFT_ALGO_AUTO) algo = dm || dm64 ? BCFFT_ALGO_DFT : BCFFT_ALGO_STAT;
+  if (algo == BCFFT_ALGO_DFTX && !dm) return BCFFT_ERR_BLOCK;
+  if (algo == BCFFT_ALGO_DFT && !dm && !dm64) return BCFFT_ERR_BLOCK;
   if (n_tokens == 0) return BCFFT_OK;
   if (!x || !h || !spectra_gu) return BCFFT_ERR_ARG;
   if (!aligned16(x) || !aligned16(h) || !aligned16(spectra_gu)) return BCFFT_ERR_ALIGN;
   if (algo == BCFFT_ALGO_STAT)
     bcfft::launch_forward_glu(block_size, n_in, x_dtype, x, n_tokens, n_gate, spectra_gu, h, (hipStream_t)stream);
+  else if (block_size == 64)
+    bcfft::launch_forward_dm64(x, n_tokens, n_gate, spectra_gu, nullptr, BCFFT_NONE, h, true, (hipStream_t)stream);
   else
     bcfft::launch_forward_dm_glu(block_size, n_in, x_dtype, algo == BCFFT_ALGO_DFTX, x, n_tokens, n_gate, spectra_gu,
                                  h, (hipStream_t)stream);

@@ -26,7 +26,10 @@ _TABLE = os.path.join(os.path.dirname(__file__), "..", "llama-fft_amd", "csrc", 
 
 def dm_table():
     """F[t][col] * 2^-7 (64 x 128) exactly as the kernel's fp16 table holds it."""
-    words = [int(w, 16) for w in re.findall(r"0x([0-9a-f]{8})u", open(_TABLE).read())]
+    text = open(_TABLE).read()
+    body = text[text.index("kDmF[4096]"):]
+    body = body[:body.index("};")]
+    words = [int(w, 16) for w in re.findall(r"0x([0-9a-f]{8})u", body)]
     w = np.array(words, dtype=np.uint32).reshape(64, 64)
     bits = np.empty((64, 128), dtype=np.uint16)
     bits[:, 0::2] = (w & 0xFFFF).astype(np.uint16)

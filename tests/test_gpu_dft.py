@@ -38,6 +38,9 @@ CASES = [
     (11008, 9, "float32", "float32", True),
     (1024, 23, "float32", "float32", False),      # a single partial group (32 of 8 blocks)
     (4096, 2000, "float32", "float32", False),    # > 1 tile per workgroup on every CU
+    (4096, 19, "bfloat16", "bfloat16", True),     # 8-token kernel: bf16 bias, ragged last tile
+    (4096, 1, "bfloat16", "bfloat16", False),     # 8-token kernel: one token, 7 empty slots
+    (1024, 9, "bfloat16", "bfloat16", True),      # 8-token kernel: one partial group
 ]
 
 
@@ -144,3 +147,31 @@ def test_dft8_bf16_matches_numpy_model(dev):
     assert rel_err(g, mdl) < 1e-3
     for t in range(x.shape[0]):
         assert rel_err(g[t], ref[t]) < 4e-3, t
+
+
+CASES64 = [
+    # (M, N, bias): b = 64 with K = 4096, bf16 I/O -> bc_forward_dm64_kernel (bcfft_dm64.hip)
+    (4096, 37, False),        # ragged last tile of 8
+    (11008, 19, True),        # 6 output groups, the last partial; bf16 bias
+    (2048, 1, False),         # one token, one group
+    (4096, 600, True),        # several tiles per workgroup
+]
+
+
+@pytest.mark.parametrize("m,n,bias", CASES64)
+def test_dft64_bf16_vs_oracle(dev, m, n, bias):
+    k, b = 4096, 64
+    rng = np.random.default_rng(m + n)
+    c = (rng.standard_normal((m // b, k // b, b)) * 0.01).astype(np.float32)
+    bv = (rng.standard_normal(m) * 0.1).astype(np.float32) if bias else None
+    x = rng.standard_normal((n, k)).astype(np.float32)
+    y, ref = _run(dev, x, c, bv, "bfloat16", "bfloat16", algo="dft")
+    _check(y, ref, "bfloat16")
+    ya, _ = _run(dev, x, c, bv, "bfloat16", "bfloat16", algo="auto")
+    assert torch.equal(y, ya)                    # AUTO resolves to it
+    x[0] *= 300.0                                # per-(token, quarter) scales: a loud token
+    x[n - 1, 1000:1100] *= 1e-3
+    y, ref = _run(dev, x, c, bv, "bfloat16", "bfloat16", algo="dft")
+    g = y.float().cpu().numpy()
+    for t in (0, n - 1):
+        assert rel_err(g[t], ref[t]) < 4e-3, (t, rel_err(g[t], ref[t]))

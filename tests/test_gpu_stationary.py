@@ -89,8 +89,8 @@ def test_stationary_vs_oracle(dev, k, m, b, n, xdt, mdt, bias):
 
 
 def test_auto_resolution_for_eligible_shapes(dev):
-    """AUTO picks the DFT-on-MFMA kernel at 4096^2 b=128 and the stationary kernel at b=64:
-    same bits as the explicit algorithm."""
+    """AUTO picks the DFT-on-MFMA kernel at 4096^2 b=128, and at b=64 the stationary kernel for
+    fp32 I/O and the b=64 DFT kernel for bf16 I/O: same bits as the explicit algorithm."""
     rng = np.random.default_rng(1)
     c = (rng.standard_normal((32, 32, 128)) * 0.01).astype(np.float32)
     x = rng.standard_normal((12, 4096)).astype(np.float32)
@@ -101,6 +101,9 @@ def test_auto_resolution_for_eligible_shapes(dev):
     ya, _ = _run(dev, x, c64, None, "float32", "float32", algo="auto")
     ys, _ = _run(dev, x, c64, None, "float32", "float32", algo="stationary")
     assert torch.equal(ya, ys)
+    ya, _ = _run(dev, x, c64, None, "bfloat16", "bfloat16", algo="auto")    # bf16 I/O at b = 64: DFT
+    yd, _ = _run(dev, x, c64, None, "bfloat16", "bfloat16", algo="dft")
+    assert torch.equal(ya, yd)
 
 
 def test_stationary_per_token_scale(dev):

@@ -237,6 +237,87 @@ def accesses_dm8():
     assert f_off % 256 == 0
 
 
+def accesses_dm64():
+    """bc_forward_dm64_kernel (bcfft_dm64.hip): b = 64, 8 token slots of 8,256 B"""
+    slot8, region8 = 8192 + 64, 8 * (8192 + 64)
+    f_off = 2 * region8
+
+    def fsw64(t):
+        return (((t >> 1) & 1) << 1) | (((t >> 3) & 1) << 2)
+
+    def xunit64(ks, f, q):
+        return 2048 * ks + 64 * (f ^ ((f >> 2) & 1)) + 16 * q
+
+    def yhalf64(w, o, par):
+        return 2048 * par + 256 * w + 8 * (o ^ (16 * ((w >> 1) & 1)))
+    for reg in (0, 1):
+        rb = reg * region8
+        for w in range(8):
+            slot = rb + w * slot8
+            for h in range(4):
+                for pt in (0, 1):
+                    yield "dm64 s1 x read", "rd128", [slot + (16 * h + (l & 15)) * 128 + 16 * (((l >> 4) + 4 * pt) ^ (l & 7))
+                                                      for l in range(64)]
+                for pr in (0, 1):
+                    for mt in (0, 1):
+                        for sec in (0, 1):
+                            ad = []
+                            for l in range(64):
+                                g, q4, p4 = l >> 4, (l & 15) >> 2, l & 3
+                                r = 8 * g + q4 + 4 * sec
+                                ad.append(f_off + 128 * r + 8 * (p4 & 1) + 16 * ((4 * pr + 2 * mt + (p4 >> 1)) ^ fsw64(r)))
+                            yield "dm64 s1 table tr read", "rd64", ad
+                        for bb in (0, 1):
+                            ad = []
+                            for l in range(64):
+                                b16, g = l & 15, l >> 4
+                                a = slot + 2048 * h + 256 * g + 64 * (pr ^ (g & 1)) + 4 * b16 + 1024 * mt + 128 * bb
+                                assert a - slot == xunit64(h, 16 * mt + 4 * g + pr + 2 * bb, b16 >> 2) + 4 * (b16 & 3)
+                                ad.append(a)
+                            yield "dm64 s1 X write", "wr32", ad
+            for fb in range(4):
+                for ks in range(4):
+                    ad = []
+                    for l in range(64):
+                        t, kb = (l & 15) >> 1, l >> 4
+                        sw = 64 * (w & 1)
+                        a = rb + t * slot8 + 256 * w + 16 * kb + (sw if fb % 2 == 0 else -sw) + 64 * fb + 2048 * ks
+                        assert a - rb - t * slot8 == xunit64(ks, 4 * w + fb, kb)
+                        ad.append(a)
+                    yield "dm64 s2 X read", "rd128", ad
+            for s2 in (0, 1):
+                for nt in (0, 1):
+                    for par in (0, 1):
+                        yield "dm64 s2 Y write", "wr64", [rb + (2 * (l >> 4) + s2) * slot8 + yhalf64(w, 16 * nt + (l & 15), par)
+                                                          for l in range(64)]
+            for pr in (0, 1):
+                for nt in (0, 1):
+                    for e in (0, 1):
+                        yield "dm64 s3 Y read", "rd64", [slot + yhalf64(2 * (l >> 4) + e, 16 * nt + (l & 15), pr) for l in range(64)]
+            for mt in (0, 1):
+                for pr in (0, 1):
+                    yield "dm64 s3 table read", "rd128", [f_off + 128 * (16 * mt + (l & 15)) + 16 * ((4 * pr + (l >> 4)) ^ fsw64(16 * mt + (l & 15)))
+                                                          for l in range(64)]
+                for nt in (0, 1):
+                    for hf in (0, 1):
+                        yield "dm64 s3 y staging write", "wr64", [slot + 128 * (16 * nt + (l & 15)) + 8 * ((4 * mt + (l >> 4) + 8 * hf) ^ (l & 15))
+                                                                  for l in range(64)]
+            for q in range(4):
+                ad = []
+                for l in range(64):
+                    rr = 8 * q + (l >> 3)
+                    ad.append(slot + 128 * rr + 16 * ((l & 7) ^ ((rr & 15) >> 1)))
+                yield "dm64 s3 y staging read", "rd128", ad
+    # the staging read returns row rr's logical 8-B units (2w, 2w+1), halves swapped when rr is odd
+    for rr in range(32):
+        for w in range(8):
+            phys = {(v ^ (rr & 15)): v for v in range(16)}
+            lo, hi = phys[2 * (w ^ ((rr & 15) >> 1))], phys[2 * (w ^ ((rr & 15) >> 1)) + 1]
+            assert (lo, hi) == ((2 * w, 2 * w + 1) if rr % 2 == 0 else (2 * w + 1, 2 * w))
+    # every Y half-unit a stage-3 lane reads was written by the wave owning those bins
+    assert f_off % 256 == 0
+
+
 def main():
     bad = 0
     for es in (4, 2):
@@ -249,7 +330,7 @@ def main():
             print(f"es={es} {name:22s} {'conflict-free' if c == 1 else f'{c}-way'}")
             bad += c > 1
     seen = {}
-    for name, kind, ad in accesses_dm8():
+    for name, kind, ad in list(accesses_dm8()) + list(accesses_dm64()):
         seen[name] = max(seen.get(name, 1), worst(ad, kind))
     for name, c in seen.items():
         print(f"bf16 {name:22s} {'conflict-free' if c == 1 else f'{c}-way'}")
