@@ -461,6 +461,11 @@ __host__ __device__ inline bool stat_eligible(int n_in, int b) {
   return (b == 128 && n_in == 32) || (b == 64 && (n_in == 32 || n_in == 64));
 }
 constexpr int STAT_OUT_BLOCKS = 32;    // output blocks per stationary group (two 16-wide N-tiles)
+// streamed-weight DFT kernel geometries (bcfft_dmk.hip): b = 128 with K > 4096. The same 16-B
+// header, then per output group of 32 blocks, per 16-block K-chunk, per wave (4), per bin of
+// the wave (16), per N-tile (2), per lane: the fp16 B fragment the lane loads for that chunk
+__host__ __device__ inline bool dmk_geometry(int n_in, int b) { return b == 128 && n_in > 32; }
+constexpr int DMK_FRAGS_PER_CHUNK = 4 * 16 * 2;   // waves x bins per wave x N-tiles
 __host__ __device__ inline SpecLayout spec_layout(int n_out, int n_in, int b) {
   SpecLayout s;
   const int h = b / 2;
@@ -483,6 +488,10 @@ __host__ __device__ inline SpecLayout spec_layout(int n_out, int n_in, int b) {
     s.stat_groups = (n_out + STAT_OUT_BLOCKS - 1) / STAT_OUT_BLOCKS;
     s.stat_pieces = (h / 8) * (n_in / 16) * 2;          // bins/wave x K-steps x N-tiles
     s.stat_u32 = 4 + (int64_t)s.stat_groups * 8 * s.stat_pieces * 64 * 4;
+  } else if (dmk_geometry(n_in, b)) {
+    s.stat_groups = (n_out + STAT_OUT_BLOCKS - 1) / STAT_OUT_BLOCKS;
+    s.stat_pieces = (n_in + 15) / 16 * DMK_FRAGS_PER_CHUNK;   // fragments per group
+    s.stat_u32 = 4 + (int64_t)s.stat_groups * s.stat_pieces * 64 * 4;
   } else {
     s.stat_groups = 0;
     s.stat_pieces = 0;
@@ -513,6 +522,14 @@ void launch_forward_dm64(const void* x, int64_t n, int n_out, const void* spec, 
                          void* y, bool glu, hipStream_t s);
 void launch_forward_dm8(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt, void* y,
                         bool glu, hipStream_t s);
+// streamed-weight DFT kernel (bcfft_dmk.hip): b = 128, K > 4096, bf16 x and bf16 y
+bool dmk_eligible(int n_in, int b, int xdt, bool yf32);
+#ifndef BCFFT_DMK_MIN_TOKENS
+#define BCFFT_DMK_MIN_TOKENS 32      // AUTO picks the streamed-weight kernel from this many tokens
+#endif
+void launch_forward_dmk(const void* x, int64_t n, int n_in, int n_out, const void* spec, const void* bias,
+                        int bias_dt, void* y, hipStream_t s);
+void launch_dmk_image(int n_out, int n_in, void* spec, hipStream_t s);
 
 // weight prep (bcfft_prep.hip): loss-aware circulant projection of a dense (n_out*b, n_in*b)
 // weight into c (n_out, n_in, b) fp32; false for an unsupported block size

@@ -1,0 +1,565 @@
+// bcfft_dmk.hip — the DFT-on-MFMA block-circulant forward for K > 4096 at b = 128, bf16 I/O
+// (gfx950): the LLaMA down projection 11008 -> 4096 and every other wide-input layer.
+//
+// Same operator as the other DFT kernels (BlockCirculantLinear.forward, patch_llama_fft.py:
+// 226-275; per block src/fft_utils.py:3-34) and the same three matrix-core stages: forward
+// block DFT (stage 1), per-bin complex MAC (stage 2), inverse block DFT (stage 3). What changes
+// is where the weights live. An output group's fp16 spectra at K = 11008 are 704 KiB: more than
+// the register file and the LDS together, so they cannot stay resident as in bcfft_dm8.hip.
+// Instead the K axis is cut into 16-block chunks and each chunk's B fragments are streamed from
+// L2 into VGPRs once per M-tile of 8 tokens, while the per-bin products accumulate in the
+// registers over all chunks.
+//
+//  * Workgroup: 8 waves (two per SIMD), persistent, one per CU. Wave w owns the 8 bins
+//    8w .. 8w + 7 and keeps Y of the tile's 8 tokens for them: 8 bins x 2 N-tiles (16 output
+//    blocks) of fp32 accumulators, rows (token, re/im) = 64 registers.
+//  * Per chunk step: wave w streams x of token w (16 blocks, 4 KiB of bf16) into LDS one step
+//    ahead (LDS-DMA), loads its 16 B fragments of the chunk (64 VGPRs, buffer loads) and runs
+//    stage 1 of its token; barrier; stage 2 of all 8 tokens on its bins; barrier.
+//  * Tile end: Y as fp16 units into the last chunk's region; stage 3 of token w (y staged in
+//    LDS, 1 KiB stores) runs at the start of the next tile.
+//  * Numerics: per-(token, chunk) power-of-two scales from stage 1. Stage 2 aligns each chunk
+//    to the token's loudest chunk so far: A rows are multiplied by 2^-d (exact, no fp16
+//    overflow), and when a later chunk is louder the token's accumulator rows are scaled down
+//    once. a, d, X and Y are one RNE fp16 term each, C and the table one term each, fp32
+//    accumulation: the bf16 kernel's numerics (tests/dm_model.py, single_x).
+//
+// LDS (148,608 B): two regions of 8 slots of 8,256 B (Y units and y staging; the x chunks of
+// a step use 4,160-B slots at the region start), the DFT table, the scales. Slot strides are
+// 64 B off the 256-B bank period, as in bcfft_dm8.hip, so the stage-2 reads of eight tokens at
+// once are conflict-free; all in-slot offsets are bcfft_dm8.hip's.
+#include "bcfft_device.h"
+#include "bcfft_dm_table.h"
+#include "bcfft_dm_common.h"
+
+namespace bcfft {
+
+namespace dmk {
+using namespace dmh;
+
+constexpr int B = 128, TT = 8, NW = 8, BPW = 8, NT = 2, MT = 1, NOG = 32;
+constexpr int XSLOT = 4096 + 64;                    // one token's 16-block x chunk -> X units
+constexpr int YSLOT = 8192 + 64;                    // one token's Y units -> y staging
+constexpr int REGION = TT * YSLOT;                  // x slots use its first TT * XSLOT bytes
+constexpr int F_OFF = 2 * REGION;                   // DFT table image, 64 rows x 256 B
+constexpr int SC_OFF = F_OFF + 16384;               // chunk scale exponents [8 tokens]
+constexpr int RR_OFF = SC_OFF + 64;                 // per-token reference exponents [8]
+constexpr int LDS_BYTES = RR_OFF + 64;
+static_assert(TT * XSLOT <= REGION, "x slots fit a region");
+static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+static_assert(F_OFF % 256 == 0, "table rows on the bank period");
+static_assert(XSLOT % 256 == 64 && YSLOT % 256 == 64, "slot strides 64 B off the bank period");
+constexpr int FRAGS = BPW * NT;                     // B fragments per wave and chunk
+
+// fp16 factor 2^-d as a (lo, hi) pair: subnormal below 2^-14, zero below 2^-24
+__device__ __forceinline__ uint32_t f16_pow2_neg(int d) {
+  return d <= 14 ? (uint32_t)(15 - d) << 10 : (d <= 24 ? 1u << (24 - d) : 0u);
+}
+}  // namespace dmk
+
+__global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
+    const void* __restrict__ xv, int64_t n_tokens, int n_in, int n_out, const uint32_t* __restrict__ stat,
+    const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
+  using namespace dmk;
+  constexpr int XT = BCFFT_BF16;
+  constexpr int ES = 2, ESY = 2;
+
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  int* wsc = reinterpret_cast<int*>(lds + SC_OFF);
+  int* wrr = reinterpret_cast<int*>(lds + RR_OFF);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n_groups = (n_out + NOG - 1) / NOG;
+  const int grp_o = blockIdx.x % n_groups;
+  const int wg_in_grp = blockIdx.x / n_groups;
+  const int64_t K = (int64_t)n_in * B;
+  const int64_t M = (int64_t)n_out * B;
+  const int nch = (n_in + 15) / 16;
+  const int64_t n_mtiles = (n_tokens + TT - 1) / TT;
+  const int gstride = (gridDim.x - grp_o + n_groups - 1) / n_groups;
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+  const uint4* bimg = reinterpret_cast<const uint4*>(stat + 4);
+
+  // ---- x chunk c of token `wave` of M-tile m -> their slots by LDS-DMA. The
+  // buffer range ends at the token's row end (a partial last chunk reads zeros) and is empty
+  // for tokens past n_tokens or tiles past the end, which then land as zeros. Piece q of a
+  // token = block rows 4q + (lane >> 4), with the slot's unit swizzle (unit u of block row r at
+  // u ^ r) applied to the global source offsets.
+  auto dma_chunk = [&](int64_t m, int c, char* region) {
+    const int dl = opaque(lane);
+    int vb[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = dl >> 4;
+      vb[q] = r * 256 + 16 * ((dl & 15) ^ ((4 * q + r) & 15));
+    }
+    {
+      const int64_t tok = m * TT + wave;
+      const bool ok = m < n_mtiles && tok < n_tokens;
+      const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<char*>((const char*)xv) + (ok ? tok * K * ES + (int64_t)c * 4096 : 0), 0,
+          ok ? (int)(K * ES - (int64_t)c * 4096) : 0, 0x00020000);
+      const uint32_t dst0 = lds_base + (uint32_t)(region - lds) + wave * XSLOT;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(vb[q]), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
+      }
+    }
+  };
+
+  // ---- the wave's 32 B fragments of chunk c (bins 16 wave + fb, N-tiles nt), from L2
+  // (buffer loads: one lane offset and SGPR piece offsets, no 64-bit address per fragment)
+  auto load_b = [&](int c, uint4 (&breg)[BPW][NT]) {
+    const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint4*>(bimg + ((int64_t)(grp_o * nch + c) * NW + wave) * FRAGS * 64), 0, FRAGS * 1024, 0x00020000);
+    const int vo = opaque(lane) * 16;
+#pragma unroll
+    for (int fb = 0; fb < BPW; ++fb)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        breg[fb][nt] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(brs, vo, (fb * NT + nt) * 1024, 0));
+  };
+
+  // ---- stage 1 (wave w, token w): x rows -> X units (one fp16 term), in place;
+  // bcfft_dm8.hip's stage 1 on one 16-block half
+  auto stage1 = [&](char* region) {
+    const int l = opaque(lane);
+    const int b16 = l & 15, g = l >> 4;
+    const int q4 = (l & 15) >> 2, p4 = l & 3;
+    const int cx = (p4 >> 1) ^ fsw(8 * g + q4);
+    const int trb = F_OFF + 256 * (8 * g + q4) + 8 * (p4 & 1);
+    int xwb[2];
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) xwb[pr] = 256 * g + 64 * (pr ^ (g & 1)) + 4 * b16;
+    {
+      char* slot = region + wave * XSLOT;
+      float xv8[2][2][8];
+      const char* rowp = slot + b16 * (B * ES);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt) {
+          const int u = 4 * ks + g + 8 * pt;
+          const uint4 w = *reinterpret_cast<const uint4*>(rowp + 16 * (u ^ b16));
+          const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float2 f = unpack16<XT>(ww[e]);
+            xv8[ks][pt][2 * e] = f.x;
+            xv8[ks][pt][2 * e + 1] = f.y;
+          }
+        }
+      float m0 = 0.f, m1 = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+          for (int j = 0; j < 8; j += 4) {
+            m0 = amax3(m0, xv8[ks][pt][j], xv8[ks][pt][j + 1]);
+            m1 = amax3(m1, xv8[ks][pt][j + 2], xv8[ks][pt][j + 3]);
+          }
+      const float mxf = __builtin_fmaxf(m0, m1);
+      const int sx = stat_scale_exp(2.f * __uint_as_float(wave_umax(__float_as_uint(mxf))));   // |a|, |d| <= 2 max|x|
+      if (l == 0) wsc[wave] = sx - 7;       // X = D 2^-(sx - 7): the table's 2^-7
+      const float S = __int_as_float((sx + 127) << 23);
+      f32x4 acc[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        uint32_t ah[4], dh[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float u0 = xv8[ks][1][2 * e] * S, u1 = xv8[ks][1][2 * e + 1] * S;
+          ah[e] = pk_rne(fmaf(xv8[ks][0][2 * e], S, u0), fmaf(xv8[ks][0][2 * e + 1], S, u1));
+          dh[e] = pk_rne(fmaf(xv8[ks][0][2 * e], S, -u0), fmaf(xv8[ks][0][2 * e + 1], S, -u1));
+        }
+        const f16x8 bah = frag(ah[0], ah[1], ah[2], ah[3]), bdh = frag(dh[0], dh[1], dh[2], dh[3]);
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) {
+            const int cb = 16 * ((8 * pr + 2 * mt) ^ cx);
+            const char* p0 = lds + trb + 256 * 32 * ks + cb;
+            const s16x4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p0));
+            const s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p0 + 256 * 4));
+            const f16x8 af = __builtin_bit_cast(f16x8, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+            acc[4 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, pr ? bdh : bah, acc[4 * pr + mt], 0, 0, 0);
+          }
+      }
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          *reinterpret_cast<uint32_t*>(slot + xwb[pr] + 1024 * mt) = pk_rne(acc[4 * pr + mt][0], acc[4 * pr + mt][1]);
+          *reinterpret_cast<uint32_t*>(slot + xwb[pr] + 1024 * mt + 128) = pk_rne(acc[4 * pr + mt][2], acc[4 * pr + mt][3]);
+        }
+    }
+  };
+
+  // accumulators of the tile: [bin of the wave][M-tile][N-tile], rows 4 yt + r = token
+  // 8 mt + 2 yt + (r >> 1), re/im r & 1; and the reference exponents of the lane's tokens
+  f32x4 acc[BPW][MT][NT];
+  int ra[MT];                                       // A-row token 8 mt + (lane & 15) / 2
+  int rc[MT][2];                                    // accumulator-row tokens 8 mt + 2 yt + s
+
+  // ---- stage 2 (all waves): per-bin complex MAC of chunk c on bins 16 wave + fb for all 8
+  // tokens. A rows (token, re/im): re rows [Xr, Xi] per block, im rows [Xi, -Xr] (v_perm +
+  // v_pk_mul_f16, which also aligns the chunk to the token's reference exponent); bin 0 (X0,
+  // X64) with the extra 1/2.
+  auto stage2 = [&](char* region, const uint4 (&breg)[BPW][NT], auto first_tag) {
+    constexpr bool FIRST = decltype(first_tag)::value;
+    const int ml = opaque(lane);
+    const int arow = ml & 15, kb = ml >> 4;
+    const int a_tl = arow >> 1, a_reim = arow & 1;
+    const uint32_t a_sel = a_reim ? 0x01000302u : 0x03020100u;
+    const int yt = ml >> 4;
+    int nka[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      nka[mt] = wsc[8 * mt + a_tl];
+      const int n0 = wsc[8 * mt + 2 * yt], n1 = wsc[8 * mt + 2 * yt + 1];
+      if constexpr (FIRST) {
+        ra[mt] = nka[mt];
+        rc[mt][0] = n0;
+        rc[mt][1] = n1;
+      } else {
+        ra[mt] = min(ra[mt], nka[mt]);
+      }
+    }
+    if constexpr (!FIRST) {
+      // a chunk louder than the token's reference: its accumulator rows scale down once
+      float fct[MT][2];
+      bool need = false;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int nn = wsc[8 * mt + 2 * yt + s];
+          const int d = rc[mt][s] - nn;
+          fct[mt][s] = d > 0 ? __builtin_ldexpf(1.f, -d) : 1.f;
+          need |= d > 0;
+          rc[mt][s] = min(rc[mt][s], nn);
+        }
+      if (__builtin_amdgcn_ballot_w64(need)) {
+#pragma unroll
+        for (int fb = 0; fb < BPW; ++fb)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) acc[fb][mt][nt][r] *= fct[mt][r >> 1];
+      }
+    }
+    uint32_t amul[MT], amul0[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int d = nka[mt] - ra[mt];               // >= 0: factor 2^-d
+      const uint32_t hh = f16_pow2_neg(d);
+      const uint32_t h0 = f16_pow2_neg(d + 1);      // bin 0: the inverse's 1/b vs 2/b
+      amul[mt] = a_reim ? (hh | ((hh | 0x8000u) << 16)) : (hh | (hh << 16));
+      amul0[mt] = a_reim ? (h0 << 16) : h0;
+    }
+    const char* ab = region + a_tl * XSLOT + 512 * wave + 16 * kb;
+#pragma unroll
+    for (int fb = 0; fb < BPW; ++fb) {
+      const int f = wave * BPW + fb;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        uint4 raw = *reinterpret_cast<const uint4*>(ab + 8 * XSLOT * mt + 64 * (fb ^ ((fb >> 2) & 1)));
+        if (f == 0) {
+          raw.x = pkmul(raw.x, amul0[mt]); raw.y = pkmul(raw.y, amul0[mt]);
+          raw.z = pkmul(raw.z, amul0[mt]); raw.w = pkmul(raw.w, amul0[mt]);
+        } else {
+          raw.x = pkmul(__builtin_amdgcn_perm(raw.x, raw.x, a_sel), amul[mt]);
+          raw.y = pkmul(__builtin_amdgcn_perm(raw.y, raw.y, a_sel), amul[mt]);
+          raw.z = pkmul(__builtin_amdgcn_perm(raw.z, raw.z, a_sel), amul[mt]);
+          raw.w = pkmul(__builtin_amdgcn_perm(raw.w, raw.w, a_sel), amul[mt]);
+        }
+        const f16x8 a = __builtin_bit_cast(f16x8, raw);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const f16x8 bf = __builtin_bit_cast(f16x8, breg[fb][nt]);
+          if constexpr (FIRST)
+            acc[fb][mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          else
+            acc[fb][mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bf, acc[fb][mt][nt], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  // ---- Y of the tile's 8 tokens (M-tile MTI) as fp16 units into the region's 8 Y slots:
+  // bcfft_dm8.hip's Y units
+  auto ywrite = [&](char* region, auto mt_tag) {
+    constexpr int MTI = decltype(mt_tag)::value;
+    const int ml = opaque(lane);
+    const int yt = ml >> 4;
+    constexpr float YS = 1.f / 2097152.f;            // 2^-21: |Y| <= n_in 2^9 < 65504 (n_in <= 127)
+    if (wave == 0 && (ml & 15) == 0) {
+      wrr[8 * MTI + 2 * yt] = rc[MTI][0];
+      wrr[8 * MTI + 2 * yt + 1] = rc[MTI][1];
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      char* yb = region + (2 * yt + s2) * YSLOT + 512 * wave + 16 * (ml & 15);
+#pragma unroll
+      for (int par = 0; par < 2; ++par)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          uint32_t u[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f32x4 a = acc[par + 2 * j][MTI][nt];
+            u[j] = pk_rne(a[2 * s2] * YS, a[2 * s2 + 1] * YS);
+          }
+          *reinterpret_cast<uint4*>(yb + 4096 * par + 256 * nt) = make_uint4(u[0], u[1], u[2], u[3]);
+        }
+    }
+  };
+
+  // ---- stage 3 (wave w, Y slot tl of a region): Y -> y rows staged in the slot and
+  // stored as 1 KiB buffer stores; bcfft_dm8.hip's stage 3. tok < 0: nothing is stored.
+  auto stage3 = [&](char* region, int tl, int rref, int64_t tok) {
+    const int l = opaque(lane);
+    const int o16 = l & 15, g = l >> 4;
+    char* slot = region + tl * YSLOT;
+    const float ysc = __builtin_ldexpf(__uint_as_float(stat[1]), 30 - rref);
+    uint4 yf[2][2][NT];
+    const char* yb = slot + 512 * g + 16 * o16;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          yf[ks][pr][nt] = *reinterpret_cast<const uint4*>(yb + 4096 * pr + 2048 * ks + 256 * nt);
+    const int gx = g ^ fsw(o16);
+    const char* gb = lds + F_OFF + 256 * o16;
+    auto gload = [&](int mt, f16x8 (&gf)[2][2]) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr)
+          gf[ks][pr] = *reinterpret_cast<const f16x8*>(gb + 4096 * mt + 16 * ((8 * pr + 4 * ks) ^ gx));
+    };
+    f16x8 gcur[2][2], gnxt[2][2];
+    gload(0, gcur);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // Y is in registers: the slot is free
+    const bool tok_ok = tok >= 0 && tok < n_tokens;
+    const int nvalid = n_out - grp_o * NOG;
+    int swb[4];
+    {
+      const int sg = ((o16 & 7) << 1) | (o16 >> 3);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) swb[mt] = 256 * o16 + 8 * ((4 * mt + g) ^ sg);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      if (mt < 3) gload(mt + 1, gnxt);
+      f32x4 E[NT], O[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        E[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        O[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          E[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][0], __builtin_bit_cast(f16x8, yf[ks][0][nt]), E[nt], 0, 0, 0);
+          O[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][1], __builtin_bit_cast(f16x8, yf[ks][1][nt]), O[nt], 0, 0, 0);
+        }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int o = 16 * nt + o16;
+        float os[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) os[r] = O[nt][r] * ysc;
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = hf ? fmaf(E[nt][r], ysc, -os[r]) : fmaf(E[nt][r], ysc, os[r]);
+          if (bias_dt != BCFFT_NONE) {              // .to(x dtype) :266, + bias :270-271
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = round_to(v[r], XT);
+            if (o < nvalid) {
+              const int64_t cc = (int64_t)(grp_o * NOG + o) * B + 16 * mt + 4 * g + 64 * hf;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] += load_scalar(bias, cc + r, bias_dt);
+            }
+          }
+          *reinterpret_cast<uint2*>(slot + 4096 * nt + swb[mt] + 128 * hf) =
+              make_uint2(pack16<XT>(v[0], v[1]), pack16<XT>(v[2], v[3]));
+        }
+      }
+      if (mt < 3) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int pr = 0; pr < 2; ++pr) gcur[ks][pr] = gnxt[ks][pr];
+      }
+    }
+    constexpr int RB = B * ESY;
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (char*)yv + (tok_ok ? tok : 0) * M * ESY + (int64_t)grp_o * NOG * RB, 0,
+        tok_ok ? (int)((M - (int64_t)grp_o * NOG * B) * ESY) : 0, 0x00020000);
+    const int w = l & 15, lr = l >> 4;
+    const int vofs = lr * RB + 16 * w;
+    int rdb[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) rdb[c] = lr * RB + 16 * ((w ^ lr) ^ (4 * c));
+    uint4 d[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      uint4 v = *reinterpret_cast<const uint4*>(slot + 1024 * q + rdb[q & 1]);
+      if (q & 2) v = make_uint4(v.z, v.w, v.x, v.y);
+      d[q] = v;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs, vofs + q * 1024, 0, 0);
+  };
+
+  // ---- prologue: the first tile's chunk 0, the DFT table
+  dma_chunk(wg_in_grp, 0, lds);
+  {
+    const uint4* tab = reinterpret_cast<const uint4*>(kDmF);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int c = tid + 512 * r;                  // chunk c: row c >> 4, chunk c & 15
+      const int t = c >> 4, ch = c & 15;
+      *reinterpret_cast<uint4*>(lds + F_OFF + 256 * t + 16 * (ch ^ fsw(t))) = tab[c];
+    }
+  }
+  wait_vmcnt<0>();
+  lds_barrier();
+
+  // Pipeline per M-tile m (region r holds its chunk 0; the other region the previous tile's
+  // Y units), two barriers per chunk step and one per tile:
+  //   step 0   stage 3 of the previous tile's token w                                | B0 |
+  //            DMA x(1) into the other region, B(0), stage 1                        | Ba |
+  //            stage 2                                                              | Bb |
+  //   step c   DMA x(c + 1) (or the next tile's chunk 0) into the other region, B(c),
+  //            stage 1                                                              | Ba |
+  //            stage 2                                                              | Bb |
+  //   end      Y units into the last chunk's region                                 | Bc |
+  // Every wave streams and transforms its own token, so x needs no barrier of its own.
+  // VMEM order per step is x DMA, then B loads, so the compiler's wait on B (it does not see
+  // the asm DMA) never drains a younger DMA.
+  int rsel = 0;
+  int64_t mprev = -1;
+  uint4 breg[BPW][NT];
+  for (int64_t m = wg_in_grp; m < n_mtiles; m += gstride) {
+    // ---- step 0
+    {
+      char* region = lds + rsel * REGION;
+      char* other = lds + (rsel ^ 1) * REGION;
+      stage3(other, wave, wrr[wave], mprev >= 0 ? mprev * TT + wave : -1);
+      lds_barrier();                                // B0: the other region is free
+      dma_chunk(m, 1, other);
+      wait_vmcnt<12>();                             // x(0) (older than 8 stores and x(1))
+      load_b(0, breg);
+      stage1(region);
+      lds_barrier();                                // Ba
+      stage2(region, breg, std::true_type{});
+      lds_barrier();                                // Bb
+      rsel ^= 1;
+    }
+    // ---- steps 1 .. nch - 1
+    for (int c = 1; c < nch; ++c) {
+      char* region = lds + rsel * REGION;
+      char* other = lds + (rsel ^ 1) * REGION;
+      wait_vmcnt<0>();                              // x(c)
+      if (c + 1 < nch) dma_chunk(m, c + 1, other);
+      else dma_chunk(m + gstride, 0, other);        // zero-filled past the last tile
+      load_b(c, breg);
+      stage1(region);
+      lds_barrier();                                // Ba
+      stage2(region, breg, std::false_type{});
+      lds_barrier();                                // Bb
+      rsel ^= 1;
+    }
+    // ---- tile end: the last chunk's region takes the Y units
+    ywrite(lds + (rsel ^ 1) * REGION, std::integral_constant<int, 0>{});
+    lds_barrier();                                  // Bc
+    mprev = m;
+  }
+  // ---- epilogue: stage 3 of the last tile
+  {
+    char* last = lds + (rsel ^ 1) * REGION;
+    stage3(last, wave, wrr[wave], mprev * TT + wave);
+  }
+}
+
+// one thread per (group, chunk, wave, bin, N-tile, lane) 16-B fragment: 4 input blocks x
+// (re, im) fp16 of conj(S) * s_C (bin 0: (S_0, S_H) * s_C), zero outside the operator
+__global__ void bc_dmk_image_kernel(int n_out, int n_in, float2* __restrict__ spec) {
+  using namespace dmk;
+  constexpr int H = B / 2;
+  const SpecLayout sl = spec_layout(n_out, n_in, B);
+  const int nch = (n_in + 15) / 16;
+  const int64_t total = (int64_t)sl.stat_groups * sl.stat_pieces * 64;
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(spec) + sl.stat_off_u32;
+  uint4* img = reinterpret_cast<uint4*>(hdr + 4);
+  const float sc = __uint_as_float(hdr[0]);
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(idx & 63);
+    const int64_t rest = idx >> 6;
+    const int nt = (int)(rest % NT);
+    const int fb = (int)((rest / NT) % BPW);
+    const int w = (int)((rest / FRAGS) % NW);
+    const int c = (int)((rest / (FRAGS * NW)) % nch);
+    const int gq = (int)(rest / (FRAGS * NW) / nch);
+    const int f = w * BPW + fb;
+    const int o = gq * NOG + nt * 16 + (lane & 15);
+    const int i0 = c * 16 + 4 * (lane >> 4);
+    uint32_t d[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int i = i0 + e;
+      float2 cv = make_float2(0.f, 0.f);
+      if (o < n_out && i < n_in) {
+        cv = spec[((int64_t)o * n_in + i) * H + f];
+        if (f != 0) cv.y = -cv.y;
+      }
+      const f16x2 h = {(_Float16)(cv.x * sc), (_Float16)(cv.y * sc)};
+      d[e] = __builtin_bit_cast(uint32_t, h);
+    }
+    img[idx] = make_uint4(d[0], d[1], d[2], d[3]);
+  }
+}
+
+bool dmk_eligible(int n_in, int b, int xdt, bool yf32) {
+  // n_in <= 127: Y = acc 2^-21 stays below fp16's max (n_in 2^30 2^-21 < 65504)
+  return dmk_geometry(n_in, b) && n_in <= 127 && xdt == BCFFT_BF16 && !yf32;
+}
+
+void launch_forward_dmk(const void* x, int64_t n, int n_in, int n_out, const void* spec, const void* bias,
+                        int bias_dt, void* y, hipStream_t s) {
+  const int groups = (n_out + dmk::NOG - 1) / dmk::NOG;
+  const SpecLayout sl = spec_layout(n_out, n_in, 128);
+  const int64_t n_mtiles = (n + dmk::TT - 1) / dmk::TT;
+  int64_t total = device_cu_count();
+  if (total > groups * n_mtiles) total = groups * n_mtiles;
+  if (total < groups) total = groups;
+  const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
+  hipLaunchKernelGGL(bc_forward_dmk_kernel, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat, bias,
+                     bias_dt, y);
+}
+
+void launch_dmk_image(int n_out, int n_in, void* spec, hipStream_t s) {
+  const SpecLayout sl = spec_layout(n_out, n_in, 128);
+  const int64_t total = (int64_t)sl.stat_groups * sl.stat_pieces * 64;
+  const unsigned blocks = (unsigned)((total + 255) / 256 < 65535 ? (total + 255) / 256 : 65535);
+  hipLaunchKernelGGL(bc_dmk_image_kernel, dim3(blocks), dim3(256), 0, s, n_out, n_in, (float2*)spec);
+}
+
+}  // namespace bcfft

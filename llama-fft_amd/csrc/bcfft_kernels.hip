@@ -734,9 +734,13 @@ int bcfft_spectra(const void* c, int c_dtype, int n_out_blocks, int n_in_blocks,
 }
 
 // the algorithm bcfft_forward_algo runs for this geometry (AUTO resolved)
-static int resolve_algo(int algo, int n_in, int block_size, int xdt = -1, bool yf32 = true) {
+// (n_tokens < 0: unknown, as for the workspace query, whose DFT choices take no workspace)
+static int resolve_algo(int algo, int n_in, int block_size, int xdt = -1, bool yf32 = true, int64_t n_tokens = -1) {
   if (algo != BCFFT_ALGO_AUTO) return algo;
   if (bcfft::dm_eligible(n_in, block_size) || bcfft::dm64_eligible(n_in, block_size, xdt, yf32)) return BCFFT_ALGO_DFT;
+  // K > 4096 at b = 128 (bf16): the streamed-weight DFT kernel from BCFFT_DMK_MIN_TOKENS up; below
+  // it the split-K MFMA kernel fills the chip better
+  if (bcfft::dmk_eligible(n_in, block_size, xdt, yf32) && n_tokens >= BCFFT_DMK_MIN_TOKENS) return BCFFT_ALGO_DFT;
   return bcfft::stat_eligible(n_in, block_size) ? BCFFT_ALGO_STAT
                                                 : (block_size <= 128 ? BCFFT_ALGO_MFMA : BCFFT_ALGO_VALU);
 }
@@ -780,12 +784,17 @@ int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_featur
   if (algo == BCFFT_ALGO_STAT && !stat_ok) return BCFFT_ERR_BLOCK;
   const bool dm64 = bcfft::dm64_eligible(n_in, block_size, x_dtype, y_dtype == BCFFT_F32);
   if (algo == BCFFT_ALGO_DFTX && !bcfft::dm_eligible(n_in, block_size)) return BCFFT_ERR_BLOCK;
-  if (algo == BCFFT_ALGO_DFT && !bcfft::dm_eligible(n_in, block_size) && !dm64) return BCFFT_ERR_BLOCK;
-  algo = resolve_algo(algo, n_in, block_size, x_dtype, y_dtype == BCFFT_F32);
+  const bool dmk = bcfft::dmk_eligible(n_in, block_size, x_dtype, y_dtype == BCFFT_F32);
+  if (algo == BCFFT_ALGO_DFT && !bcfft::dm_eligible(n_in, block_size) && !dm64 && !dmk) return BCFFT_ERR_BLOCK;
+  algo = resolve_algo(algo, n_in, block_size, x_dtype, y_dtype == BCFFT_F32, n_tokens);
   // the workspace is used only when it is as large as bcfft_forward_workspace_bytes asks
   const int64_t need = bcfft_forward_workspace_bytes(n_tokens, in_features, out_features, block_size, algo);
   float* ws = (workspace && need > 0 && workspace_bytes >= need) ? (float*)workspace : nullptr;
   hipStream_t s = (hipStream_t)stream;
+  if (algo == BCFFT_ALGO_DFT && dmk) {
+    bcfft::launch_forward_dmk(x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, s);
+    return record_launch();
+  }
   if (algo == BCFFT_ALGO_DFT && block_size == 64) {
     bcfft::launch_forward_dm64(x, n_tokens, n_out, spectra, bias, bias_dtype, y, false, s);
     return record_launch();

@@ -1100,6 +1100,11 @@ bool launch_forward_stat(int b, int n_in, int xdt, bool yf32, const void* x, int
 }
 
 void launch_stat_image(int b, int n_out, int n_in, void* spec, hipStream_t s) {
+  if (dmk_geometry(n_in, b)) {                      // same header, streamed per-chunk fragments
+    hipLaunchKernelGGL(bc_stat_scale_kernel<128>, dim3(1), dim3(1024), 0, s, n_out, n_in, (float2*)spec);
+    launch_dmk_image(n_out, n_in, spec, s);
+    return;
+  }
   if (!stat_eligible(n_in, b)) return;
   const SpecLayout sl = spec_layout(n_out, n_in, b);
   const int64_t total = (int64_t)sl.stat_groups * 8 * sl.stat_pieces * 64;

@@ -1,0 +1,94 @@
+"""GPU parity of the streamed-weight DFT kernel (bcfft_dmk.hip: b = 128, K > 4096, bf16 I/O;
+the LLaMA down projection 11008 -> 4096) against the CPU oracle.
+
+Numerics are the 8-token bf16 kernel's (tests/dm_model.py, single_x): per-(token, chunk)
+power-of-two scales, a/d, X and Y one RNE fp16 term each, C and the table one term each, fp32
+accumulation; chunks are aligned to each token's loudest chunk so far, and accumulator rows are
+scaled down when a later chunk is louder. Outputs are bf16: within ~1 output ulp plus the norm
+bound (_check), as every bf16 case of the other DFT kernels."""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import rel_err
+from oracle import bc_oracle as O
+from test_gpu_stationary import _check, _run
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    import bcfft
+    bcfft.load()
+    return torch.device("cuda:0")
+
+
+CASES = [
+    # (K, M, N, bias)
+    (11008, 4096, 37, False),      # down projection: 86 input blocks = 6 chunks, the last of 6
+    (11008, 4096, 1, False),       # one token: 7 empty slots in the tile
+    (11008, 4096, 300, True),      # many tiles per workgroup; bf16 bias
+    (5120, 1024, 17, True),        # 40 input blocks (last chunk of 8), one partial output group
+    (6144, 5120, 50, False),       # 48 input blocks (3 full chunks), 2 groups, the last partial
+    (16256, 512, 9, False),        # 127 input blocks: the largest K the kernel takes
+]
+
+
+@pytest.mark.parametrize("k,m,n,bias", CASES)
+def test_dmk_bf16_vs_oracle(dev, k, m, n, bias):
+    b = 128
+    rng = np.random.default_rng(k + m + n)
+    c = (rng.standard_normal((m // b, k // b, b)) * 0.01).astype(np.float32)
+    bv = (rng.standard_normal(m) * 0.1).astype(np.float32) if bias else None
+    x = rng.standard_normal((n, k)).astype(np.float32)
+    y, ref = _run(dev, x, c, bv, "bfloat16", "bfloat16", algo="dft")
+    _check(y, ref, "bfloat16")
+    if n >= 32:                                   # AUTO resolves to it from 32 tokens
+        ya, _ = _run(dev, x, c, bv, "bfloat16", "bfloat16", algo="auto")
+        assert torch.equal(y, ya)
+
+
+def test_dmk_per_token_chunk_scales(dev):
+    """Chunks of one token at very different magnitudes, in both orders (a later louder chunk
+    scales the accumulated rows down), zero and tiny tokens, a single massive channel."""
+    k, m, b = 11008, 4096, 128
+    rng = np.random.default_rng(5)
+    c = (rng.standard_normal((m // b, k // b, b)) * 0.01).astype(np.float32)
+    x = rng.standard_normal((11, k)).astype(np.float32)
+    x[0, 9000:9500] *= 3e3            # chunk 4 of token 0 far louder than chunks 0-3
+    x[1, :2048] *= 3e3                # chunk 0 far louder than the rest
+    x[2] = 0.0
+    x[3] *= 1e-20
+    x[4, 10000] = 5000.0              # one massive channel in the last (partial) chunk
+    x[5, 2048:4096] *= 1e-6           # one very quiet chunk in the middle
+    x[6, 4096:] *= 1e5                # every chunk after the second louder
+    y, ref = _run(dev, x, c, None, "bfloat16", "bfloat16", algo="dft")
+    g = y.float().cpu().numpy()
+    assert np.all(g[2] == 0.0)
+    for t in range(x.shape[0]):
+        if t == 2:
+            continue
+        e = rel_err(g[t], ref[t])
+        assert e < 4e-3, (t, e)
+
+
+def test_dmk_full_size_and_linearity(dev):
+    """11008 -> 4096, N = 8192 (the sweep's down projection): oracle parity on a slice, run-to-run
+    bit equality, and linearity over all tokens within the bf16 rounding."""
+    from bcfft import ops
+    k, m, b, n = 11008, 4096, 128, 8192
+    rng = np.random.default_rng(0)
+    c = (rng.standard_normal((m // b, k // b, b)) * 0.01).astype(np.float32)
+    spec = ops.spectra(torch.from_numpy(c).to(dev).to(torch.bfloat16))
+    xt = torch.randn(n, k, device=dev).to(torch.bfloat16)
+    y = ops.forward(xt, spec, None, b, m, algo="dft")
+    sl = slice(5000, 5128)
+    ref = O.bc_forward(xt[sl].float().cpu().numpy(), O.round_to(c, O.BF16), x_dtype=O.BF16)
+    assert rel_err(y[sl].float().cpu().numpy(), ref) < 4e-3
+    assert torch.equal(y, ops.forward(xt, spec, None, b, m, algo="dft"))
+    x2 = torch.randn(n, k, device=dev).to(torch.bfloat16)
+    lhs = ops.forward((xt.float() + x2.float()).to(torch.bfloat16), spec, None, b, m, algo="dft").float()
+    rhs = y.float() + ops.forward(x2, spec, None, b, m, algo="dft").float()
+    assert ((lhs - rhs).norm() / rhs.norm()).item() < 1e-2

@@ -39,6 +39,8 @@ if __name__ == "__main__":
     shapes = [(4096, 4096, 128, "fp32", 8192), (4096, 4096, 128, "bf16", 8192), (4096, 11008, 128, "bf16", 8192),
               (4096, 4096, 64, "fp32", 8192)]
     algos = [a for a in sys.argv[1:] if not a.startswith("--")] or ["stationary", "mfma", "valu"]
+    if "--down" in sys.argv:                        # K > 4096: the streamed-weight kernel vs split-K MFMA
+        shapes = [(11008, 4096, 128, "bf16", n) for n in (16, 64, 256, 1024, 1700, 8192)]
     if "--smalln" in sys.argv:                      # AUTO's small-N crossover
         shapes = [(4096, 4096, b, io, n) for b in (64, 128) for io in ("fp32",) for n in (16, 64, 128, 256, 512, 1024, 2048)]
     for k, m, b, io, n in shapes:
