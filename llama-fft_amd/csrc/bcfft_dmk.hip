@@ -7,25 +7,28 @@
 // is where the weights live. An output group's fp16 spectra at K = 11008 are 704 KiB: more than
 // the register file and the LDS together, so they cannot stay resident as in bcfft_dm8.hip.
 // Instead the K axis is cut into 16-block chunks and each chunk's B fragments are streamed from
-// L2 into VGPRs once per M-tile of 8 tokens, while the per-bin products accumulate in the
+// L2 into VGPRs once per M-tile of 16 tokens, while the per-bin products accumulate in the
 // registers over all chunks.
 //
 //  * Workgroup: 8 waves (two per SIMD), persistent, one per CU. Wave w owns the 8 bins
-//    8w .. 8w + 7 and keeps Y of the tile's 8 tokens for them: 8 bins x 2 N-tiles (16 output
-//    blocks) of fp32 accumulators, rows (token, re/im) = 64 registers.
-//  * Per chunk step: wave w streams x of token w (16 blocks, 4 KiB of bf16) into LDS one step
-//    ahead (LDS-DMA), loads its 16 B fragments of the chunk (64 VGPRs, buffer loads) and runs
-//    stage 1 of its token; barrier; stage 2 of all 8 tokens on its bins; barrier.
-//  * Tile end: Y as fp16 units into the last chunk's region; stage 3 of token w (y staged in
-//    LDS, 1 KiB stores) runs at the start of the next tile.
+//    8w .. 8w + 7 and keeps Y of the tile's 16 tokens for them: 8 bins x 2 M-tiles (8 tokens
+//    x re/im) x 2 N-tiles (16 output blocks) of fp32 accumulators = 128 registers.
+//  * Per chunk step: wave w streams x of tokens 2w, 2w + 1 (16 blocks, 4 KiB of bf16 each)
+//    into LDS one step ahead (LDS-DMA), loads its 16 B fragments of the chunk (64 VGPRs,
+//    buffer loads) and runs stage 1 of its tokens; barrier; stage 2 of all 16 tokens on its
+//    bins; barrier. Each B fragment serves 16 tokens: the L2 -> CU stream of weights is
+//    48 KiB per token.
+//  * Tile end: Y of tokens 0-7 as fp16 units into the last chunk's region, stage 3 of token w
+//    (y staged in LDS, 1 KiB stores); then Y of tokens 8-15, whose stage 3 runs at the start
+//    of the next tile.
 //  * Numerics: per-(token, chunk) power-of-two scales from stage 1. Stage 2 aligns each chunk
 //    to the token's loudest chunk so far: A rows are multiplied by 2^-d (exact, no fp16
 //    overflow), and when a later chunk is louder the token's accumulator rows are scaled down
 //    once. a, d, X and Y are one RNE fp16 term each, C and the table one term each, fp32
 //    accumulation: the bf16 kernel's numerics (tests/dm_model.py, single_x).
 //
-// LDS (148,608 B): two regions of 8 slots of 8,256 B (Y units and y staging; the x chunks of
-// a step use 4,160-B slots at the region start), the DFT table, the scales. Slot strides are
+// LDS (149,632 B): two regions of 16 x-chunk slots of 4,160 B (8 Y / y-staging slots of
+// 8,256 B at the tile end), the DFT table, the scales. Slot strides are
 // 64 B off the 256-B bank period, as in bcfft_dm8.hip, so the stage-2 reads of eight tokens at
 // once are conflict-free; all in-slot offsets are bcfft_dm8.hip's.
 #include "bcfft_device.h"
@@ -36,20 +39,33 @@ namespace bcfft {
 
 namespace dmk {
 using namespace dmh;
+// analysis builds only (tools/ab_dmk.sh; results are WRONG when set): 1 no B loads, 2 no stage-1
+// arithmetic, 4 no stage-2 MFMAs, 8 no stage 3, 16 no x DMA
+#ifdef BCFFT_DMK_ABL
+constexpr int ABL = BCFFT_DMK_ABL;
+#else
+constexpr int ABL = 0;
+#endif
 
-constexpr int B = 128, TT = 8, NW = 8, BPW = 8, NT = 2, MT = 1, NOG = 32;
+constexpr int B = 128, NW = 8, BPW = 8, NT = 2, NOG = 32;
 constexpr int XSLOT = 4096 + 64;                    // one token's 16-block x chunk -> X units
 constexpr int YSLOT = 8192 + 64;                    // one token's Y units -> y staging
-constexpr int REGION = TT * YSLOT;                  // x slots use its first TT * XSLOT bytes
-constexpr int F_OFF = 2 * REGION;                   // DFT table image, 64 rows x 256 B
-constexpr int SC_OFF = F_OFF + 16384;               // chunk scale exponents [8 tokens]
-constexpr int RR_OFF = SC_OFF + 64;                 // per-token reference exponents [8]
-constexpr int LDS_BYTES = RR_OFF + 64;
-static_assert(TT * XSLOT <= REGION, "x slots fit a region");
-static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
-static_assert(F_OFF % 256 == 0, "table rows on the bank period");
 static_assert(XSLOT % 256 == 64 && YSLOT % 256 == 64, "slot strides 64 B off the bank period");
 constexpr int FRAGS = BPW * NT;                     // B fragments per wave and chunk
+// per tile size TT (8 or 16 tokens): M-tiles, x DMA pieces per wave and chunk, LDS map
+template <int TT>
+struct Geo {
+  static constexpr int MT = TT / 8;
+  static constexpr int TPW = TT / NW;               // tokens per wave (x DMA, stage 1)
+  static constexpr int NDMA = TPW * 4;              // 1-KiB x DMA pieces per wave and chunk
+  static constexpr int REGION = TT * XSLOT > 8 * YSLOT ? TT * XSLOT : 8 * YSLOT;   // x, or Y of 8 tokens
+  static constexpr int F_OFF = 2 * REGION;          // DFT table image, 64 rows x 256 B
+  static constexpr int SC_OFF = F_OFF + 16384;      // chunk scale exponents [TT]
+  static constexpr int RR_OFF = SC_OFF + 64;        // per-token reference exponents [TT]
+  static constexpr int LDS_BYTES = RR_OFF + 64;
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+  static_assert(F_OFF % 256 == 0, "table rows on the bank period");
+};
 
 // fp16 factor 2^-d as a (lo, hi) pair: subnormal below 2^-14, zero below 2^-24
 __device__ __forceinline__ uint32_t f16_pow2_neg(int d) {
@@ -57,16 +73,19 @@ __device__ __forceinline__ uint32_t f16_pow2_neg(int d) {
 }
 }  // namespace dmk
 
+template <int TT>
 __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_in, int n_out, const uint32_t* __restrict__ stat,
     const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
   using namespace dmk;
+  using G = Geo<TT>;
+  constexpr int MT = G::MT, TPW = G::TPW, NDMA = G::NDMA, REGION = G::REGION, F_OFF = G::F_OFF;
   constexpr int XT = BCFFT_BF16;
   constexpr int ES = 2, ESY = 2;
 
-  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
-  int* wsc = reinterpret_cast<int*>(lds + SC_OFF);
-  int* wrr = reinterpret_cast<int*>(lds + RR_OFF);
+  __shared__ __attribute__((aligned(16))) char lds[G::LDS_BYTES];
+  int* wsc = reinterpret_cast<int*>(lds + G::SC_OFF);
+  int* wrr = reinterpret_cast<int*>(lds + G::RR_OFF);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -87,6 +106,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
   // token = block rows 4q + (lane >> 4), with the slot's unit swizzle (unit u of block row r at
   // u ^ r) applied to the global source offsets.
   auto dma_chunk = [&](int64_t m, int c, char* region) {
+    if constexpr ((ABL & 16) != 0) return;
     const int dl = opaque(lane);
     int vb[4];
 #pragma unroll
@@ -94,13 +114,14 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
       const int r = dl >> 4;
       vb[q] = r * 256 + 16 * ((dl & 15) ^ ((4 * q + r) & 15));
     }
-    {
-      const int64_t tok = m * TT + wave;
+#pragma unroll
+    for (int t2 = 0; t2 < TPW; ++t2) {
+      const int64_t tok = m * TT + TPW * wave + t2;
       const bool ok = m < n_mtiles && tok < n_tokens;
       const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
           const_cast<char*>((const char*)xv) + (ok ? tok * K * ES + (int64_t)c * 4096 : 0), 0,
           ok ? (int)(K * ES - (int64_t)c * 4096) : 0, 0x00020000);
-      const uint32_t dst0 = lds_base + (uint32_t)(region - lds) + wave * XSLOT;
+      const uint32_t dst0 = lds_base + (uint32_t)(region - lds) + (TPW * wave + t2) * XSLOT;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         uint32_t keep;
@@ -110,47 +131,58 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
     }
   };
 
-  // ---- the wave's 32 B fragments of chunk c (bins 16 wave + fb, N-tiles nt), from L2
-  // (buffer loads: one lane offset and SGPR piece offsets, no 64-bit address per fragment)
-  auto load_b = [&](int c, uint4 (&breg)[BPW][NT]) {
+  // ---- the wave's B fragments of chunk c for N-tile nt (bins 8 wave + fb), from L2. Asm
+  // buffer loads like the x DMA: the compiler does not count them, so its own waits never
+  // drain the x DMA issued after them; wait_b (below) is the one wait on them, with the exact
+  // number of younger VMEM operations, and it redefines the registers it waited for, so no use
+  // can be scheduled above it.
+  auto load_b = [&](int c, int nt, u32x4 (&breg)[BPW][NT]) {
     const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint4*>(bimg + ((int64_t)(grp_o * nch + c) * NW + wave) * FRAGS * 64), 0, FRAGS * 1024, 0x00020000);
     const int vo = opaque(lane) * 16;
 #pragma unroll
-    for (int fb = 0; fb < BPW; ++fb)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-        breg[fb][nt] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(brs, vo, (fb * NT + nt) * 1024, 0));
+    for (int fb = 0; fb < BPW; ++fb) {
+      if constexpr ((ABL & 1) != 0) breg[fb][nt] = u32x4{(uint32_t)vo, (uint32_t)vo, (uint32_t)vo, (uint32_t)vo};
+      else asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen"
+                        : "=v"(breg[fb][nt]) : "v"(vo), "s"(brs), "s"((fb * NT + nt) * 1024) : "memory");
+    }
   };
+  // wait until at most N younger VMEM operations are outstanding: N. tile's fragments landed
+  auto wait_b = [&](auto n_tag, int nt, u32x4 (&breg)[BPW][NT]) {
+    constexpr int N = decltype(n_tag)::value;
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    asm volatile("s_waitcnt vmcnt(%8)"
+                 : "+v"(breg[0][nt]), "+v"(breg[1][nt]), "+v"(breg[2][nt]), "+v"(breg[3][nt]),
+                   "+v"(breg[4][nt]), "+v"(breg[5][nt]), "+v"(breg[6][nt]), "+v"(breg[7][nt])
+                 : "n"(N) : "memory");
+  };
+  static_assert(BPW == 8, "wait_b names eight fragments");
 
-  // ---- stage 1 (wave w, token w): x rows -> X units (one fp16 term), in place;
-  // bcfft_dm8.hip's stage 1 on one 16-block half
+  // ---- stage 1 (wave w, tokens 2w, 2w + 1): x rows -> X units (one fp16 term), in place;
+  // bcfft_dm8.hip's stage 1 on one 16-block half, with the x rows kept packed and the two
+  // output parities in turn (the wave's 128 accumulators and 64 B registers stay live)
   auto stage1 = [&](char* region) {
+    if constexpr ((ABL & 2) != 0) {
+      if (lane < TPW) wsc[TPW * wave + lane] = 0;
+      return;
+    }
     const int l = opaque(lane);
     const int b16 = l & 15, g = l >> 4;
     const int q4 = (l & 15) >> 2, p4 = l & 3;
     const int cx = (p4 >> 1) ^ fsw(8 * g + q4);
     const int trb = F_OFF + 256 * (8 * g + q4) + 8 * (p4 & 1);
-    int xwb[2];
-#pragma unroll
-    for (int pr = 0; pr < 2; ++pr) xwb[pr] = 256 * g + 64 * (pr ^ (g & 1)) + 4 * b16;
-    {
-      char* slot = region + wave * XSLOT;
-      float xv8[2][2][8];
+#pragma unroll 1
+    for (int t2 = 0; t2 < TPW; ++t2) {
+      char* slot = region + (TPW * wave + t2) * XSLOT;
+      // x of block b16: t = 32 ks + 8 g + j and t + 64 (j < 8)
       const char* rowp = slot + b16 * (B * ES);
+      uint32_t xr[2][2][4];
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int pt = 0; pt < 2; ++pt) {
-          const int u = 4 * ks + g + 8 * pt;
-          const uint4 w = *reinterpret_cast<const uint4*>(rowp + 16 * (u ^ b16));
-          const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float2 f = unpack16<XT>(ww[e]);
-            xv8[ks][pt][2 * e] = f.x;
-            xv8[ks][pt][2 * e + 1] = f.y;
-          }
+          const uint4 w = *reinterpret_cast<const uint4*>(rowp + 16 * ((4 * ks + g + 8 * pt) ^ b16));
+          xr[ks][pt][0] = w.x; xr[ks][pt][1] = w.y; xr[ks][pt][2] = w.z; xr[ks][pt][3] = w.w;
         }
       float m0 = 0.f, m1 = 0.f;
 #pragma unroll
@@ -158,46 +190,54 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
 #pragma unroll
         for (int pt = 0; pt < 2; ++pt)
 #pragma unroll
-          for (int j = 0; j < 8; j += 4) {
-            m0 = amax3(m0, xv8[ks][pt][j], xv8[ks][pt][j + 1]);
-            m1 = amax3(m1, xv8[ks][pt][j + 2], xv8[ks][pt][j + 3]);
+          for (int e = 0; e < 4; e += 2) {
+            const float2 f0 = unpack16<XT>(xr[ks][pt][e]), f1 = unpack16<XT>(xr[ks][pt][e + 1]);
+            m0 = amax3(m0, f0.x, f0.y);
+            m1 = amax3(m1, f1.x, f1.y);
           }
       const float mxf = __builtin_fmaxf(m0, m1);
       const int sx = stat_scale_exp(2.f * __uint_as_float(wave_umax(__float_as_uint(mxf))));   // |a|, |d| <= 2 max|x|
-      if (l == 0) wsc[wave] = sx - 7;       // X = D 2^-(sx - 7): the table's 2^-7
+      if (l == 0) wsc[TPW * wave + t2] = sx - 7;      // X = D 2^-(sx - 7): the table's 2^-7
       const float S = __int_as_float((sx + 127) << 23);
-      f32x4 acc[8];
+      uint32_t ah[2][4], dh[2][4];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        uint32_t ah[4], dh[4];
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float u0 = xv8[ks][1][2 * e] * S, u1 = xv8[ks][1][2 * e + 1] * S;
-          ah[e] = pk_rne(fmaf(xv8[ks][0][2 * e], S, u0), fmaf(xv8[ks][0][2 * e + 1], S, u1));
-          dh[e] = pk_rne(fmaf(xv8[ks][0][2 * e], S, -u0), fmaf(xv8[ks][0][2 * e + 1], S, -u1));
+          const float2 lo = unpack16<XT>(xr[ks][0][e]), hi = unpack16<XT>(xr[ks][1][e]);
+          const float u0 = hi.x * S, u1 = hi.y * S;
+          ah[ks][e] = pk_rne(fmaf(lo.x, S, u0), fmaf(lo.y, S, u1));
+          dh[ks][e] = pk_rne(fmaf(lo.x, S, -u0), fmaf(lo.y, S, -u1));
         }
-        const f16x8 bah = frag(ah[0], ah[1], ah[2], ah[3]), bdh = frag(dh[0], dh[1], dh[2], dh[3]);
+      // X write lane bases: D^T row 4g + r is bin 16 mt + 4 g + pr (+ 2 for r >= 2), column
+      // block b16; bin bit 2 = g & 1 swaps the 64-B blocks
 #pragma unroll
-        for (int pr = 0; pr < 2; ++pr)
+      for (int pr = 0; pr < 2; ++pr) {
+        f32x4 acc4[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc4[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const f16x8 bx = pr ? frag(dh[ks][0], dh[ks][1], dh[ks][2], dh[ks][3])
+                              : frag(ah[ks][0], ah[ks][1], ah[ks][2], ah[ks][3]);
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt) {
+            // A = F^T (16 bins-reals x 32 t): two transposed reads of 4 rows each
             const int cb = 16 * ((8 * pr + 2 * mt) ^ cx);
             const char* p0 = lds + trb + 256 * 32 * ks + cb;
             const s16x4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p0));
             const s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p0 + 256 * 4));
             const f16x8 af = __builtin_bit_cast(f16x8, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
-            acc[4 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, pr ? bdh : bah, acc[4 * pr + mt], 0, 0, 0);
+            acc4[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bx, acc4[mt], 0, 0, 0);
           }
-      }
-#pragma unroll
-      for (int pr = 0; pr < 2; ++pr)
+        }
+        const int xwb = 256 * g + 64 * (pr ^ (g & 1)) + 4 * b16;
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
-          *reinterpret_cast<uint32_t*>(slot + xwb[pr] + 1024 * mt) = pk_rne(acc[4 * pr + mt][0], acc[4 * pr + mt][1]);
-          *reinterpret_cast<uint32_t*>(slot + xwb[pr] + 1024 * mt + 128) = pk_rne(acc[4 * pr + mt][2], acc[4 * pr + mt][3]);
+          *reinterpret_cast<uint32_t*>(slot + xwb + 1024 * mt) = pk_rne(acc4[mt][0], acc4[mt][1]);
+          *reinterpret_cast<uint32_t*>(slot + xwb + 1024 * mt + 128) = pk_rne(acc4[mt][2], acc4[mt][3]);
         }
+      }
     }
   };
 
@@ -211,7 +251,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
   // tokens. A rows (token, re/im): re rows [Xr, Xi] per block, im rows [Xi, -Xr] (v_perm +
   // v_pk_mul_f16, which also aligns the chunk to the token's reference exponent); bin 0 (X0,
   // X64) with the extra 1/2.
-  auto stage2 = [&](char* region, const uint4 (&breg)[BPW][NT], auto first_tag) {
+  auto stage2 = [&](char* region, u32x4 (&breg)[BPW][NT], int cn, auto first_tag) {
     constexpr bool FIRST = decltype(first_tag)::value;
     const int ml = opaque(lane);
     const int arow = ml & 15, kb = ml >> 4;
@@ -266,31 +306,47 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
       amul0[mt] = a_reim ? (h0 << 16) : h0;
     }
     const char* ab = region + a_tl * XSLOT + 512 * wave + 16 * kb;
+    // one pass per N-tile (the A rows are read and transformed again for the second): when a
+    // pass is done, its B registers take the next chunk's fragments (cn), a whole step ahead
 #pragma unroll
-    for (int fb = 0; fb < BPW; ++fb) {
-      const int f = wave * BPW + fb;
+    for (int nt = 0; nt < NT; ++nt) {
+      // younger VMEM than this pass's fragments: the other pass's 8 (pass 0) or the prefetch's
+      // 8 (pass 1), and outside step 0 the DMA of the next chunk (NDMA)
+      if constexpr (FIRST) {
+        wait_b(std::integral_constant<int, 8>{}, nt, breg);
+      } else if (nt == 0 || cn >= 0) {
+        wait_b(std::integral_constant<int, 8 + NDMA>{}, nt, breg);
+      } else {
+        wait_b(std::integral_constant<int, NDMA>{}, nt, breg);
+      }
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        uint4 raw = *reinterpret_cast<const uint4*>(ab + 8 * XSLOT * mt + 64 * (fb ^ ((fb >> 2) & 1)));
-        if (f == 0) {
-          raw.x = pkmul(raw.x, amul0[mt]); raw.y = pkmul(raw.y, amul0[mt]);
-          raw.z = pkmul(raw.z, amul0[mt]); raw.w = pkmul(raw.w, amul0[mt]);
-        } else {
-          raw.x = pkmul(__builtin_amdgcn_perm(raw.x, raw.x, a_sel), amul[mt]);
-          raw.y = pkmul(__builtin_amdgcn_perm(raw.y, raw.y, a_sel), amul[mt]);
-          raw.z = pkmul(__builtin_amdgcn_perm(raw.z, raw.z, a_sel), amul[mt]);
-          raw.w = pkmul(__builtin_amdgcn_perm(raw.w, raw.w, a_sel), amul[mt]);
-        }
-        const f16x8 a = __builtin_bit_cast(f16x8, raw);
+      for (int fb = 0; fb < BPW; ++fb) {
+        if (fb == BPW / 2) __builtin_amdgcn_sched_barrier(0);   // bounds the hoisted A reads
+        const int f = wave * BPW + fb;
+        const f16x8 bf = __builtin_bit_cast(f16x8, breg[fb][nt]);
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-          const f16x8 bf = __builtin_bit_cast(f16x8, breg[fb][nt]);
-          if constexpr (FIRST)
+        for (int mt = 0; mt < MT; ++mt) {
+          uint4 raw = *reinterpret_cast<const uint4*>(ab + 8 * XSLOT * mt + 64 * (fb ^ ((fb >> 2) & 1)));
+          if (f == 0) {
+            raw.x = pkmul(raw.x, amul0[mt]); raw.y = pkmul(raw.y, amul0[mt]);
+            raw.z = pkmul(raw.z, amul0[mt]); raw.w = pkmul(raw.w, amul0[mt]);
+          } else {
+            raw.x = pkmul(__builtin_amdgcn_perm(raw.x, raw.x, a_sel), amul[mt]);
+            raw.y = pkmul(__builtin_amdgcn_perm(raw.y, raw.y, a_sel), amul[mt]);
+            raw.z = pkmul(__builtin_amdgcn_perm(raw.z, raw.z, a_sel), amul[mt]);
+            raw.w = pkmul(__builtin_amdgcn_perm(raw.w, raw.w, a_sel), amul[mt]);
+          }
+          const f16x8 a = __builtin_bit_cast(f16x8, raw);
+          if constexpr ((ABL & 4) != 0)
+            acc[fb][mt][nt] = FIRST ? f32x4{a[0], a[1], bf[0], bf[1]} : acc[fb][mt][nt] + f32x4{a[0], a[1], bf[0], bf[1]};
+          else if constexpr (FIRST)
             acc[fb][mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
           else
             acc[fb][mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bf, acc[fb][mt][nt], 0, 0, 0);
         }
       }
+      __builtin_amdgcn_sched_barrier(0);            // the loads reuse this pass's B registers
+      if (cn >= 0) load_b(cn, nt, breg);
     }
   };
 
@@ -326,6 +382,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
   // ---- stage 3 (wave w, Y slot tl of a region): Y -> y rows staged in the slot and
   // stored as 1 KiB buffer stores; bcfft_dm8.hip's stage 3. tok < 0: nothing is stored.
   auto stage3 = [&](char* region, int tl, int rref, int64_t tok) {
+    if constexpr ((ABL & 8) != 0) return;
     const int l = opaque(lane);
     const int o16 = l & 15, g = l >> 4;
     char* slot = region + tl * YSLOT;
@@ -428,6 +485,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
   };
 
   // ---- prologue: the first tile's chunk 0, the DFT table
+  u32x4 breg[BPW][NT];
   dma_chunk(wg_in_grp, 0, lds);
   {
     const uint4* tab = reinterpret_cast<const uint4*>(kDmF);
@@ -441,34 +499,36 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
   wait_vmcnt<0>();
   lds_barrier();
 
-  // Pipeline per M-tile m (region r holds its chunk 0; the other region the previous tile's
-  // Y units), two barriers per chunk step and one per tile:
-  //   step 0   stage 3 of the previous tile's token w                                | B0 |
+  // Pipeline per M-tile m of 16 tokens (region r holds its chunk 0; the other region the
+  // previous tile's Y units of tokens 8-15), two barriers per chunk step:
+  //   step 0   stage 3 of the previous tile's token 8 + w                           | B0 |
   //            DMA x(1) into the other region, B(0), stage 1                        | Ba |
-  //            stage 2                                                              | Bb |
-  //   step c   DMA x(c + 1) (or the next tile's chunk 0) into the other region, B(c),
+  //            stage 2 on B(0), loading B(1) N-tile by N-tile                       | Bb |
+  //   step c   DMA x(c + 1) (or the next tile's chunk 0) into the other region,
   //            stage 1                                                              | Ba |
-  //            stage 2                                                              | Bb |
-  //   end      Y units into the last chunk's region                                 | Bc |
-  // Every wave streams and transforms its own token, so x needs no barrier of its own.
-  // VMEM order per step is x DMA, then B loads, so the compiler's wait on B (it does not see
-  // the asm DMA) never drains a younger DMA.
+  //            stage 2 on B(c), loading B(c + 1) unless c is the last chunk         | Bb |
+  //   end      Y(tokens 0-7) into the last region | Bc | stage 3 of token w           | Bd |
+  //            Y(tokens 8-15)                                                       | Be |
+  // Every wave streams and transforms its own two tokens, so x needs no barrier of its own.
+  // VMEM order is x DMA of step c, then the B loads for step c + 1, so the compiler's waits on
+  // B (it does not see the asm DMA) drain at most that one DMA, a stage 1 after its issue.
   int rsel = 0;
   int64_t mprev = -1;
-  uint4 breg[BPW][NT];
+  constexpr int LH = MT - 1;                        // the half tile whose stage 3 is deferred
   for (int64_t m = wg_in_grp; m < n_mtiles; m += gstride) {
     // ---- step 0
     {
       char* region = lds + rsel * REGION;
       char* other = lds + (rsel ^ 1) * REGION;
-      stage3(other, wave, wrr[wave], mprev >= 0 ? mprev * TT + wave : -1);
+      stage3(other, wave, wrr[8 * LH + wave], mprev >= 0 ? mprev * TT + 8 * LH + wave : -1);
       lds_barrier();                                // B0: the other region is free
       dma_chunk(m, 1, other);
-      wait_vmcnt<12>();                             // x(0) (older than 8 stores and x(1))
-      load_b(0, breg);
+      wait_vmcnt<8 * MT + NDMA>();                  // x(0): older than the stage-3 stores and x(1)
+      load_b(0, 0, breg);                           // B(0): not carried across the tile end,
+      load_b(0, 1, breg);                           // where stage 3 needs the registers
       stage1(region);
       lds_barrier();                                // Ba
-      stage2(region, breg, std::true_type{});
+      stage2(region, breg, 1, std::true_type{});
       lds_barrier();                                // Bb
       rsel ^= 1;
     }
@@ -476,26 +536,29 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
     for (int c = 1; c < nch; ++c) {
       char* region = lds + rsel * REGION;
       char* other = lds + (rsel ^ 1) * REGION;
-      wait_vmcnt<0>();                              // x(c)
+      wait_vmcnt<16>();                             // x(c) (older than B(c))
       if (c + 1 < nch) dma_chunk(m, c + 1, other);
       else dma_chunk(m + gstride, 0, other);        // zero-filled past the last tile
-      load_b(c, breg);
       stage1(region);
       lds_barrier();                                // Ba
-      stage2(region, breg, std::false_type{});
+      stage2(region, breg, c + 1 < nch ? c + 1 : -1, std::false_type{});
       lds_barrier();                                // Bb
       rsel ^= 1;
     }
-    // ---- tile end: the last chunk's region takes the Y units
-    ywrite(lds + (rsel ^ 1) * REGION, std::integral_constant<int, 0>{});
-    lds_barrier();                                  // Bc
+    // ---- tile end: the last chunk's region takes the Y units, 8 tokens at a time
+    char* last = lds + (rsel ^ 1) * REGION;
+    if constexpr (MT == 2) {
+      ywrite(last, std::integral_constant<int, 0>{});
+      lds_barrier();                                // Bc
+      stage3(last, wave, wrr[wave], m * TT + wave);
+      lds_barrier();                                // Bd: staging reads of tokens 0-7 done
+    }
+    ywrite(last, std::integral_constant<int, LH>{});
+    lds_barrier();                                  // Be
     mprev = m;
   }
-  // ---- epilogue: stage 3 of the last tile
-  {
-    char* last = lds + (rsel ^ 1) * REGION;
-    stage3(last, wave, wrr[wave], mprev * TT + wave);
-  }
+  // ---- epilogue: the last tile's deferred half
+  stage3(lds + (rsel ^ 1) * REGION, wave, wrr[8 * LH + wave], mprev * TT + 8 * LH + wave);
 }
 
 // one thread per (group, chunk, wave, bin, N-tile, lane) 16-B fragment: 4 input blocks x
@@ -546,13 +609,21 @@ void launch_forward_dmk(const void* x, int64_t n, int n_in, int n_out, const voi
                         int bias_dt, void* y, hipStream_t s) {
   const int groups = (n_out + dmk::NOG - 1) / dmk::NOG;
   const SpecLayout sl = spec_layout(n_out, n_in, 128);
-  const int64_t n_mtiles = (n + dmk::TT - 1) / dmk::TT;
-  int64_t total = device_cu_count();
+  const int64_t cus = device_cu_count();
+  const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
+  // 16-token tiles halve the weight stream per token; 8-token tiles finish a tile in about half
+  // the time, so they win while 16-token tiles would leave CUs idle
+  const bool t16 = groups * ((n + 15) / 16) >= cus;
+  const int64_t n_mtiles = t16 ? (n + 15) / 16 : (n + 7) / 8;
+  int64_t total = cus;
   if (total > groups * n_mtiles) total = groups * n_mtiles;
   if (total < groups) total = groups;
-  const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
-  hipLaunchKernelGGL(bc_forward_dmk_kernel, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat, bias,
-                     bias_dt, y);
+  if (t16)
+    hipLaunchKernelGGL(bc_forward_dmk_kernel<16>, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat,
+                       bias, bias_dt, y);
+  else
+    hipLaunchKernelGGL(bc_forward_dmk_kernel<8>, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat,
+                       bias, bias_dt, y);
 }
 
 void launch_dmk_image(int n_out, int n_in, void* spec, hipStream_t s) {

@@ -25,6 +25,18 @@ def dev():
     return torch.device("cuda:0")
 
 
+def _extremes(rng, k):
+    x = rng.standard_normal((11, k)).astype(np.float32)
+    x[0, 9000:9500] *= 3e3            # chunk 4 of token 0 far louder than chunks 0-3
+    x[1, :2048] *= 3e3                # chunk 0 far louder than the rest
+    x[2] = 0.0
+    x[3] *= 1e-20
+    x[4, 10000] = 5000.0              # one massive channel in the last (partial) chunk
+    x[5, 2048:4096] *= 1e-6           # one very quiet chunk in the middle
+    x[6, 4096:] *= 1e5                # every chunk after the second louder
+    return x
+
+
 CASES = [
     # (K, M, N, bias)
     (11008, 4096, 37, False),      # down projection: 86 input blocks = 6 chunks, the last of 6
@@ -50,20 +62,30 @@ def test_dmk_bf16_vs_oracle(dev, k, m, n, bias):
         assert torch.equal(y, ya)
 
 
-def test_dmk_per_token_chunk_scales(dev):
+@pytest.mark.parametrize("n", [11, 4100])
+def test_dmk_per_token_chunk_scales(dev, n):
     """Chunks of one token at very different magnitudes, in both orders (a later louder chunk
-    scales the accumulated rows down), zero and tiny tokens, a single massive channel."""
+    scales the accumulated rows down), zero and tiny tokens, a single massive channel. n = 11
+    runs 8-token tiles; n = 4100 fills every CU with 16-token tiles (the last one ragged)."""
+    from bcfft import ops
     k, m, b = 11008, 4096, 128
     rng = np.random.default_rng(5)
     c = (rng.standard_normal((m // b, k // b, b)) * 0.01).astype(np.float32)
-    x = rng.standard_normal((11, k)).astype(np.float32)
-    x[0, 9000:9500] *= 3e3            # chunk 4 of token 0 far louder than chunks 0-3
-    x[1, :2048] *= 3e3                # chunk 0 far louder than the rest
-    x[2] = 0.0
-    x[3] *= 1e-20
-    x[4, 10000] = 5000.0              # one massive channel in the last (partial) chunk
-    x[5, 2048:4096] *= 1e-6           # one very quiet chunk in the middle
-    x[6, 4096:] *= 1e5                # every chunk after the second louder
+    if n > 11:                                    # oracle on the special rows and the ragged tail
+        x = rng.standard_normal((n, k)).astype(np.float32)
+        x[:11] = _extremes(rng, k)
+        spec = ops.spectra(torch.from_numpy(c).to(dev).to(torch.bfloat16))
+        xt = torch.from_numpy(x).to(dev).to(torch.bfloat16)
+        y = ops.forward(xt, spec, None, b, m, algo="dft").float().cpu().numpy()
+        rows = list(range(11)) + list(range(n - 20, n))
+        xr = xt[rows].float().cpu().numpy()
+        ref = O.bc_forward(xr, O.round_to(c, O.BF16), x_dtype=O.BF16)
+        assert np.all(y[2] == 0.0)
+        for i, t in enumerate(rows):
+            if t != 2:
+                assert rel_err(y[t], ref[i]) < 4e-3, (t, rel_err(y[t], ref[i]))
+        return
+    x = _extremes(rng, k)
     y, ref = _run(dev, x, c, None, "bfloat16", "bfloat16", algo="dft")
     g = y.float().cpu().numpy()
     assert np.all(g[2] == 0.0)

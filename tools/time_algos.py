@@ -41,6 +41,8 @@ if __name__ == "__main__":
     algos = [a for a in sys.argv[1:] if not a.startswith("--")] or ["stationary", "mfma", "valu"]
     if "--down" in sys.argv:                        # K > 4096: the streamed-weight kernel vs split-K MFMA
         shapes = [(11008, 4096, 128, "bf16", n) for n in (16, 64, 256, 1024, 1700, 8192)]
+    if "--down2" in sys.argv:
+        shapes = [(11008, 4096, 128, "bf16", n) for n in (1700, 8192)]
     if "--smalln" in sys.argv:                      # AUTO's small-N crossover
         shapes = [(4096, 4096, b, io, n) for b in (64, 128) for io in ("fp32",) for n in (16, 64, 128, 256, 512, 1024, 2048)]
     for k, m, b, io, n in shapes:
