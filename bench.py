@@ -57,6 +57,9 @@ def resolved_kernel(algo, k, b, io="fp32"):
     if io == "bf16" and algo in ("dft", "auto") and dft_ok:
         return ("dft", "bc_forward_dm8_kernel",
                 "MFMA fp16 throughout, 8 tokens per tile, one-term spectra (bf16 I/O)")
+    if io == "bf16" and algo in ("dft", "auto") and b == 128 and 32 < n_in <= 127:   # N >= 32 (bench: 8192)
+        return ("dft", "bc_forward_dmk_kernel",
+                "MFMA fp16 throughout, 16-block K-chunks with weight fragments streamed from L2 (bf16 I/O)")
     if algo == "dftx":
         return ("dftx", "bc_forward_dm_kernel",
                 "MFMA fp16 throughout: block DFT (even/odd split, x hi+lo) x 2^-7 table, stationary "
