@@ -67,7 +67,12 @@ struct Geo {
   static_assert(F_OFF % 256 == 0, "table rows on the bank period");
 };
 
-// fp16 factor 2^-d as a (lo, hi) pair: subnormal below 2^-14, zero below 2^-24
+// chunk alignment headroom: stage 1 keeps |X| below 2^(14 - HEAD), so stage 2 can raise a chunk
+// up to 2^HEAD louder than the token's reference exponent without an fp16 overflow, and the
+// accumulator rescale runs only for chunks beyond that (never for chunk maxima that differ by
+// less than 16x, i.e. practically never for activations without outliers)
+constexpr int HEAD = 4;
+// fp16 factor 2^-d (d >= -15) as a (lo, hi) pair: subnormal below 2^-14, zero below 2^-24
 __device__ __forceinline__ uint32_t f16_pow2_neg(int d) {
   return d <= 14 ? (uint32_t)(15 - d) << 10 : (d <= 24 ? 1u << (24 - d) : 0u);
 }
@@ -99,6 +104,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
   const int gstride = (gridDim.x - grp_o + n_groups - 1) / n_groups;
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
   const uint4* bimg = reinterpret_cast<const uint4*>(stat + 4);
+#ifdef BCFFT_STAMPS
+  ANALYSIS_INIT;
+  (void)ablate_flags_;
+#endif
 
   // ---- x chunk c of token `wave` of M-tile m -> their slots by LDS-DMA. The
   // buffer range ends at the token's row end (a partial last chunk reads zeros) and is empty
@@ -136,16 +145,23 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
   // drain the x DMA issued after them; wait_b (below) is the one wait on them, with the exact
   // number of younger VMEM operations, and it redefines the registers it waited for, so no use
   // can be scheduled above it.
+  auto b_rsrc = [&](int c) {                        // c < 0: an empty range (loads return 0)
+    return __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint4*>(bimg + ((int64_t)(grp_o * nch + (c < 0 ? 0 : c)) * NW + wave) * FRAGS * 64), 0,
+        c < 0 ? 0 : FRAGS * 1024, 0x00020000);
+  };
+  // fragment (fb, nt); no memory clobber: the asm only writes its register, so LDS reads may
+  // be scheduled across it (both asm statements are volatile, so load and wait keep their order)
+  auto load_b1 = [&](const __amdgpu_buffer_rsrc_t& brs, int vo, int fb, int nt, u32x4 (&breg)[BPW][NT]) {
+    if constexpr ((ABL & 1) != 0) breg[fb][nt] = u32x4{(uint32_t)vo, (uint32_t)vo, (uint32_t)vo, (uint32_t)vo};
+    else asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen"
+                      : "=v"(breg[fb][nt]) : "v"(vo), "s"(brs), "s"((fb * NT + nt) * 1024));
+  };
   auto load_b = [&](int c, int nt, u32x4 (&breg)[BPW][NT]) {
-    const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint4*>(bimg + ((int64_t)(grp_o * nch + c) * NW + wave) * FRAGS * 64), 0, FRAGS * 1024, 0x00020000);
+    const __amdgpu_buffer_rsrc_t brs = b_rsrc(c);
     const int vo = opaque(lane) * 16;
 #pragma unroll
-    for (int fb = 0; fb < BPW; ++fb) {
-      if constexpr ((ABL & 1) != 0) breg[fb][nt] = u32x4{(uint32_t)vo, (uint32_t)vo, (uint32_t)vo, (uint32_t)vo};
-      else asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen"
-                        : "=v"(breg[fb][nt]) : "v"(vo), "s"(brs), "s"((fb * NT + nt) * 1024) : "memory");
-    }
+    for (int fb = 0; fb < BPW; ++fb) load_b1(brs, vo, fb, nt, breg);
   };
   // wait until at most N younger VMEM operations are outstanding: N. tile's fragments landed
   auto wait_b = [&](auto n_tag, int nt, u32x4 (&breg)[BPW][NT]) {
@@ -196,7 +212,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
             m1 = amax3(m1, f1.x, f1.y);
           }
       const float mxf = __builtin_fmaxf(m0, m1);
-      const int sx = stat_scale_exp(2.f * __uint_as_float(wave_umax(__float_as_uint(mxf))));   // |a|, |d| <= 2 max|x|
+      // |a|, |d| <= 2 max|x| < 2^(15 - HEAD): stage 2 may raise a chunk by up to 2^HEAD
+      const int sx = stat_scale_exp(2.f * __uint_as_float(wave_umax(__float_as_uint(mxf)))) - HEAD;
       if (l == 0) wsc[TPW * wave + t2] = sx - 7;      // X = D 2^-(sx - 7): the table's 2^-7
       const float S = __int_as_float((sx + 127) << 23);
       uint32_t ah[2][4], dh[2][4];
@@ -268,18 +285,19 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
         rc[mt][0] = n0;
         rc[mt][1] = n1;
       } else {
-        ra[mt] = min(ra[mt], nka[mt]);
+        ra[mt] = min(ra[mt], nka[mt] + HEAD);
       }
     }
     if constexpr (!FIRST) {
-      // a chunk louder than the token's reference: its accumulator rows scale down once
+      // a chunk more than 2^HEAD louder than the token's reference: the reference drops to the
+      // chunk's exponent + HEAD and the token's accumulator rows scale down once
       float fct[MT][2];
       bool need = false;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          const int nn = wsc[8 * mt + 2 * yt + s];
+          const int nn = wsc[8 * mt + 2 * yt + s] + HEAD;
           const int d = rc[mt][s] - nn;
           fct[mt][s] = d > 0 ? __builtin_ldexpf(1.f, -d) : 1.f;
           need |= d > 0;
@@ -299,44 +317,43 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
     uint32_t amul[MT], amul0[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      const int d = nka[mt] - ra[mt];               // >= 0: factor 2^-d
+      const int d = nka[mt] - ra[mt];               // >= -HEAD: factor 2^-d <= 2^HEAD
       const uint32_t hh = f16_pow2_neg(d);
       const uint32_t h0 = f16_pow2_neg(d + 1);      // bin 0: the inverse's 1/b vs 2/b
       amul[mt] = a_reim ? (hh | ((hh | 0x8000u) << 16)) : (hh | (hh << 16));
       amul0[mt] = a_reim ? (h0 << 16) : h0;
     }
     const char* ab = region + a_tl * XSLOT + 512 * wave + 16 * kb;
-    // one pass per N-tile (the A rows are read and transformed again for the second): when a
-    // pass is done, its B registers take the next chunk's fragments (cn), a whole step ahead
+    // B of this chunk (prefetched bin by bin in the previous step): younger VMEM is, outside
+    // step 0, the next chunk's x DMA (NDMA)
+    if constexpr (FIRST) {
+      wait_b(std::integral_constant<int, 0>{}, 0, breg);
+      wait_b(std::integral_constant<int, 0>{}, 1, breg);
+    } else {
+      wait_b(std::integral_constant<int, NDMA>{}, 0, breg);
+      wait_b(std::integral_constant<int, NDMA>{}, 1, breg);
+    }
+    const __amdgpu_buffer_rsrc_t nbrs = b_rsrc(cn);
+    const int vo = opaque(lane) * 16;
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      // younger VMEM than this pass's fragments: the other pass's 8 (pass 0) or the prefetch's
-      // 8 (pass 1), and outside step 0 the DMA of the next chunk (NDMA)
-      if constexpr (FIRST) {
-        wait_b(std::integral_constant<int, 8>{}, nt, breg);
-      } else if (nt == 0 || cn >= 0) {
-        wait_b(std::integral_constant<int, 8 + NDMA>{}, nt, breg);
-      } else {
-        wait_b(std::integral_constant<int, NDMA>{}, nt, breg);
-      }
+    for (int fb = 0; fb < BPW; ++fb) {
+      const int f = wave * BPW + fb;
 #pragma unroll
-      for (int fb = 0; fb < BPW; ++fb) {
-        if (fb == BPW / 2) __builtin_amdgcn_sched_barrier(0);   // bounds the hoisted A reads
-        const int f = wave * BPW + fb;
-        const f16x8 bf = __builtin_bit_cast(f16x8, breg[fb][nt]);
+      for (int mt = 0; mt < MT; ++mt) {
+        uint4 raw = *reinterpret_cast<const uint4*>(ab + 8 * XSLOT * mt + 64 * (fb ^ ((fb >> 2) & 1)));
+        if (f == 0) {
+          raw.x = pkmul(raw.x, amul0[mt]); raw.y = pkmul(raw.y, amul0[mt]);
+          raw.z = pkmul(raw.z, amul0[mt]); raw.w = pkmul(raw.w, amul0[mt]);
+        } else {
+          raw.x = pkmul(__builtin_amdgcn_perm(raw.x, raw.x, a_sel), amul[mt]);
+          raw.y = pkmul(__builtin_amdgcn_perm(raw.y, raw.y, a_sel), amul[mt]);
+          raw.z = pkmul(__builtin_amdgcn_perm(raw.z, raw.z, a_sel), amul[mt]);
+          raw.w = pkmul(__builtin_amdgcn_perm(raw.w, raw.w, a_sel), amul[mt]);
+        }
+        const f16x8 a = __builtin_bit_cast(f16x8, raw);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          uint4 raw = *reinterpret_cast<const uint4*>(ab + 8 * XSLOT * mt + 64 * (fb ^ ((fb >> 2) & 1)));
-          if (f == 0) {
-            raw.x = pkmul(raw.x, amul0[mt]); raw.y = pkmul(raw.y, amul0[mt]);
-            raw.z = pkmul(raw.z, amul0[mt]); raw.w = pkmul(raw.w, amul0[mt]);
-          } else {
-            raw.x = pkmul(__builtin_amdgcn_perm(raw.x, raw.x, a_sel), amul[mt]);
-            raw.y = pkmul(__builtin_amdgcn_perm(raw.y, raw.y, a_sel), amul[mt]);
-            raw.z = pkmul(__builtin_amdgcn_perm(raw.z, raw.z, a_sel), amul[mt]);
-            raw.w = pkmul(__builtin_amdgcn_perm(raw.w, raw.w, a_sel), amul[mt]);
-          }
-          const f16x8 a = __builtin_bit_cast(f16x8, raw);
+        for (int nt = 0; nt < NT; ++nt) {
+          const f16x8 bf = __builtin_bit_cast(f16x8, breg[fb][nt]);
           if constexpr ((ABL & 4) != 0)
             acc[fb][mt][nt] = FIRST ? f32x4{a[0], a[1], bf[0], bf[1]} : acc[fb][mt][nt] + f32x4{a[0], a[1], bf[0], bf[1]};
           else if constexpr (FIRST)
@@ -345,8 +362,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
             acc[fb][mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bf, acc[fb][mt][nt], 0, 0, 0);
         }
       }
-      __builtin_amdgcn_sched_barrier(0);            // the loads reuse this pass's B registers
-      if (cn >= 0) load_b(cn, nt, breg);
+      // this bin's fragments of the next chunk (cn < 0: none; an empty range) into the same
+      // registers, a whole step ahead of their use; spread over the bins, not one burst
+      load_b1(nbrs, vo, fb, 0, breg);
+      load_b1(nbrs, vo, fb, 1, breg);
     }
   };
 
@@ -498,6 +517,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
   }
   wait_vmcnt<0>();
   lds_barrier();
+  STAMP(0);
 
   // Pipeline per M-tile m of 16 tokens (region r holds its chunk 0; the other region the
   // previous tile's Y units of tokens 8-15), two barriers per chunk step:
@@ -515,21 +535,31 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
   int rsel = 0;
   int64_t mprev = -1;
   constexpr int LH = MT - 1;                        // the half tile whose stage 3 is deferred
-  for (int64_t m = wg_in_grp; m < n_mtiles; m += gstride) {
+  int tix = 0;                                      // stamps builds: tiles 0 and 1 are timed
+  for (int64_t m = wg_in_grp; m < n_mtiles; m += gstride, ++tix) {
+    const int sb = 1 + 30 * tix;
+#define DSTAMP(o) do { if (tix < 2) STAMP(sb + (o)); } while (0)
     // ---- step 0
     {
       char* region = lds + rsel * REGION;
       char* other = lds + (rsel ^ 1) * REGION;
+      DSTAMP(0);
       stage3(other, wave, wrr[8 * LH + wave], mprev >= 0 ? mprev * TT + 8 * LH + wave : -1);
+      DSTAMP(1);
       lds_barrier();                                // B0: the other region is free
+      DSTAMP(2);
       dma_chunk(m, 1, other);
       wait_vmcnt<8 * MT + NDMA>();                  // x(0): older than the stage-3 stores and x(1)
       load_b(0, 0, breg);                           // B(0): not carried across the tile end,
       load_b(0, 1, breg);                           // where stage 3 needs the registers
       stage1(region);
+      DSTAMP(3);
       lds_barrier();                                // Ba
+      DSTAMP(4);
       stage2(region, breg, 1, std::true_type{});
+      DSTAMP(5);
       lds_barrier();                                // Bb
+      DSTAMP(6);
       rsel ^= 1;
     }
     // ---- steps 1 .. nch - 1
@@ -540,9 +570,12 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
       if (c + 1 < nch) dma_chunk(m, c + 1, other);
       else dma_chunk(m + gstride, 0, other);        // zero-filled past the last tile
       stage1(region);
+      if (c <= 5) DSTAMP(7 + 3 * (c - 1));
       lds_barrier();                                // Ba
+      if (c <= 5) DSTAMP(8 + 3 * (c - 1));
       stage2(region, breg, c + 1 < nch ? c + 1 : -1, std::false_type{});
       lds_barrier();                                // Bb
+      if (c <= 5) DSTAMP(9 + 3 * (c - 1));
       rsel ^= 1;
     }
     // ---- tile end: the last chunk's region takes the Y units, 8 tokens at a time
@@ -550,15 +583,21 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
     if constexpr (MT == 2) {
       ywrite(last, std::integral_constant<int, 0>{});
       lds_barrier();                                // Bc
+      DSTAMP(22);
       stage3(last, wave, wrr[wave], m * TT + wave);
+      DSTAMP(23);
       lds_barrier();                                // Bd: staging reads of tokens 0-7 done
+      DSTAMP(24);
     }
     ywrite(last, std::integral_constant<int, LH>{});
     lds_barrier();                                  // Be
+    DSTAMP(25);
+#undef DSTAMP
     mprev = m;
   }
   // ---- epilogue: the last tile's deferred half
   stage3(lds + (rsel ^ 1) * REGION, wave, wrr[8 * LH + wave], mprev * TT + 8 * LH + wave);
+  STAMP(63);
 }
 
 // one thread per (group, chunk, wave, bin, N-tile, lane) 16-B fragment: 4 input blocks x
@@ -634,3 +673,15 @@ void launch_dmk_image(int n_out, int n_in, void* spec, hipStream_t s) {
 }
 
 }  // namespace bcfft
+
+#ifdef BCFFT_STAMPS
+// analysis build only: stamp buffer of bc_forward_dmk_kernel (this TU's copy). Slots per wave: 0
+// start | per tile t < 2 (base 1 + 30 t): +0 step 0 top, +1 stage 3 done, +2 after B0, +3 stage 1
+// done, +4 after Ba, +5 stage 2 done, +6 after Bb; step c in 1..5: +7 + 3 (c - 1) stage 1 done,
+// +8 ... after Ba, +9 ... after Bb | 16-token tiles: +22 after Bc, +23 stage 3 done, +24 after Bd |
+// +25 after Be | 63 end (tools/timeline_dmk.py)
+extern "C" int bcfft_set_stamps_dmk(void* buf) {
+  unsigned long long* p = (unsigned long long*)buf;
+  return hipMemcpyToSymbol(HIP_SYMBOL(bcfft::g_stamps), &p, sizeof(p)) == hipSuccess ? 0 : BCFFT_ERR_HIP;
+}
+#endif
