@@ -145,10 +145,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
   // drain the x DMA issued after them; wait_b (below) is the one wait on them, with the exact
   // number of younger VMEM operations, and it redefines the registers it waited for, so no use
   // can be scheduled above it.
-  auto b_rsrc = [&](int c) {                        // c < 0: an empty range (loads return 0)
+  auto b_rsrc = [&](int c) {
     return __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint4*>(bimg + ((int64_t)(grp_o * nch + (c < 0 ? 0 : c)) * NW + wave) * FRAGS * 64), 0,
-        c < 0 ? 0 : FRAGS * 1024, 0x00020000);
+        FRAGS * 1024, 0x00020000);
   };
   // fragment (fb, nt); no memory clobber: the asm only writes its register, so LDS reads may
   // be scheduled across it (both asm statements are volatile, so load and wait keep their order)
@@ -326,9 +326,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
     const char* ab = region + a_tl * XSLOT + 512 * wave + 16 * kb;
     // B of this chunk (prefetched bin by bin in the previous step): younger VMEM is, outside
     // step 0, the next chunk's x DMA (NDMA)
-    if constexpr (FIRST) {
-      wait_b(std::integral_constant<int, 0>{}, 0, breg);
-      wait_b(std::integral_constant<int, 0>{}, 1, breg);
+    if constexpr (FIRST) {                          // younger: 8 stage-3 stores and x(1)
+      wait_b(std::integral_constant<int, 8 + NDMA>{}, 0, breg);
+      wait_b(std::integral_constant<int, 8 + NDMA>{}, 1, breg);
     } else {
       wait_b(std::integral_constant<int, NDMA>{}, 0, breg);
       wait_b(std::integral_constant<int, NDMA>{}, 1, breg);
@@ -362,10 +362,14 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
             acc[fb][mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bf, acc[fb][mt][nt], 0, 0, 0);
         }
       }
-      // this bin's fragments of the next chunk (cn < 0: none; an empty range) into the same
-      // registers, a whole step ahead of their use; spread over the bins, not one burst
-      load_b1(nbrs, vo, fb, 0, breg);
-      load_b1(nbrs, vo, fb, 1, breg);
+      // this bin's fragments of the next chunk into the same registers, a whole step ahead of
+      // their use; spread over the bins, not one burst. None after the last chunk: an asm load
+      // whose result is never read leaves its registers free to the allocator while the load
+      // is still in flight
+      if (cn >= 0) {
+        load_b1(nbrs, vo, fb, 0, breg);
+        load_b1(nbrs, vo, fb, 1, breg);
+      }
     }
   };
 
@@ -521,8 +525,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
 
   // Pipeline per M-tile m of 16 tokens (region r holds its chunk 0; the other region the
   // previous tile's Y units of tokens 8-15), two barriers per chunk step:
-  //   step 0   stage 3 of the previous tile's token 8 + w                           | B0 |
-  //            DMA x(1) into the other region, B(0), stage 1                        | Ba |
+  //   step 0   B(0); stage 3 of the previous tile's deferred token                  | B0 |
+  //            DMA x(1) into the other region, stage 1                              | Ba |
   //            stage 2 on B(0), loading B(1) N-tile by N-tile                       | Bb |
   //   step c   DMA x(c + 1) (or the next tile's chunk 0) into the other region,
   //            stage 1                                                              | Ba |
@@ -544,14 +548,14 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
       char* region = lds + rsel * REGION;
       char* other = lds + (rsel ^ 1) * REGION;
       DSTAMP(0);
+      load_b(0, 0, breg);                           // B(0): issued here, not carried across the
+      load_b(0, 1, breg);                           // tile end (the accumulators are dead now)
       stage3(other, wave, wrr[8 * LH + wave], mprev >= 0 ? mprev * TT + 8 * LH + wave : -1);
       DSTAMP(1);
       lds_barrier();                                // B0: the other region is free
       DSTAMP(2);
       dma_chunk(m, 1, other);
-      wait_vmcnt<8 * MT + NDMA>();                  // x(0): older than the stage-3 stores and x(1)
-      load_b(0, 0, breg);                           // B(0): not carried across the tile end,
-      load_b(0, 1, breg);                           // where stage 3 needs the registers
+      wait_vmcnt<24 + NDMA>();                      // x(0): older than B(0), 8 stores and x(1)
       stage1(region);
       DSTAMP(3);
       lds_barrier();                                // Ba
