@@ -656,7 +656,11 @@ void launch_forward_dmk(const void* x, int64_t n, int n_in, int n_out, const voi
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
   // 16-token tiles halve the weight stream per token; 8-token tiles finish a tile in about half
   // the time, so they win while 16-token tiles would leave CUs idle
+#ifdef BCFFT_DMK_TILE
+  const bool t16 = BCFFT_DMK_TILE == 16;           // analysis builds: force a tile size
+#else
   const bool t16 = groups * ((n + 15) / 16) >= cus;
+#endif
   const int64_t n_mtiles = t16 ? (n + 15) / 16 : (n + 7) / 8;
   int64_t total = cus;
   if (total > groups * n_mtiles) total = groups * n_mtiles;
