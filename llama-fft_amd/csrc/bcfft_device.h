@@ -438,6 +438,33 @@ __device__ __forceinline__ void stage_store(float* dst, uint4 v) {
   }
 }
 
+// ------------------------------------------------------------------ persistent grids
+// Output group and tile lane of a persistent 1-D grid's workgroup, and the lane stride. When
+// the grid is a multiple of 8 x groups the map is XCD-aware: blocks are dealt round-robin over
+// the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch), so block b = 8 i + xcd takes group
+// i % groups and lane 8 (i / groups) + xcd. Every group's workgroup of one tile lane then sits
+// on the same XCD and the tile's x is fetched from HBM once, not once per group (PMC at
+// 4096 -> 11008, 3 groups: 196 -> 74 MB of reads). Otherwise group = b % groups.
+struct GroupMap { int grp, lane, stride; };
+__device__ __forceinline__ GroupMap group_map(int n_groups) {
+  const int b = blockIdx.x;
+  if (n_groups > 1 && gridDim.x % (8 * n_groups) == 0)
+    return {(b / 8) % n_groups, (b / 8 / n_groups) * 8 + b % 8, (int)gridDim.x / n_groups};
+  const int g = b % n_groups;
+  return {g, b / n_groups, ((int)gridDim.x - g + n_groups - 1) / n_groups};
+}
+// grid for group_map: one workgroup per CU, trimmed to a multiple of 8 x groups when several
+// groups share enough tiles and the trim idles at most 1/16 of the CUs (3 or 6 groups: 240 of
+// 256; 11 groups would keep only 176), never more than groups x tiles nor fewer than groups
+inline int64_t group_grid(int64_t cus, int groups, int64_t n_mtiles) {
+  int64_t total = cus;
+  const int64_t xt = cus / (8 * groups) * (8 * groups);
+  if (groups > 1 && n_mtiles * groups >= cus && xt * 16 >= cus * 15) total = xt;
+  if (total > groups * n_mtiles) total = groups * n_mtiles;
+  if (total < groups) total = groups;
+  return total;
+}
+
 // ------------------------------------------------------------------ spectra buffer layout
 // [packed fp32: nO*nI*H float2][twiddles: B float2][MFMA image (b <= 128)][stationary image]
 // MFMA image: dword ((c*H + f)*2 + prec)*nOp*8 + o*8 + j  = split-bf16 pair of bin f of

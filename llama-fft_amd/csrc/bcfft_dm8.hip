@@ -68,11 +68,11 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
   // in N-tile 0 and the matching up blocks in N-tile 1, and stores 16 h rows
   constexpr int OPG = GLU ? NOG / 2 : NOG;
   const int n_groups = (n_out + OPG - 1) / OPG;
-  const int grp_o = blockIdx.x % n_groups;
-  const int wg_in_grp = blockIdx.x / n_groups;
+  const GroupMap gm = group_map(n_groups);          // XCD-aware when the grid allows it
+  const int grp_o = gm.grp, wg_in_grp = gm.lane;
   const int64_t M = (int64_t)n_out * B;
   const int64_t n_mtiles = (n_tokens + TT - 1) / TT;
-  const int gstride = (gridDim.x - grp_o + n_groups - 1) / n_groups;
+  const int gstride = gm.stride;
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
 
   // ---- x of token `wave` of M-tile m -> its slot by LDS-DMA (the buffer range zero-fills
@@ -463,9 +463,7 @@ void launch_dm8(const void* x, int64_t n, int n_out, const void* spec, const voi
   const int groups = GLU ? (n_out + 15) / 16 : (n_out + 31) / 32;
   const bcfft::SpecLayout sl = bcfft::spec_layout(GLU ? 32 * groups : n_out, 32, 128);
   const int64_t n_mtiles = (n + 7) / 8;
-  int64_t total = bcfft::device_cu_count();
-  if (total > groups * n_mtiles) total = groups * n_mtiles;
-  if (total < groups) total = groups;
+  const int64_t total = bcfft::group_grid(bcfft::device_cu_count(), groups, n_mtiles);
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
   hipLaunchKernelGGL((bcfft::bc_forward_dm8_kernel<GLU>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_out, stat,
                      bias, bias_dt, y);

@@ -95,13 +95,13 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n_groups = (n_out + NOG - 1) / NOG;
-  const int grp_o = blockIdx.x % n_groups;
-  const int wg_in_grp = blockIdx.x / n_groups;
+  const GroupMap gm = group_map(n_groups);          // XCD-aware when the grid allows it
+  const int grp_o = gm.grp, wg_in_grp = gm.lane;
   const int64_t K = (int64_t)n_in * B;
   const int64_t M = (int64_t)n_out * B;
   const int nch = (n_in + 15) / 16;
   const int64_t n_mtiles = (n_tokens + TT - 1) / TT;
-  const int gstride = (gridDim.x - grp_o + n_groups - 1) / n_groups;
+  const int gstride = gm.stride;
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
   const uint4* bimg = reinterpret_cast<const uint4*>(stat + 4);
 #ifdef BCFFT_STAMPS
@@ -662,9 +662,7 @@ void launch_forward_dmk(const void* x, int64_t n, int n_in, int n_out, const voi
   const bool t16 = groups * ((n + 15) / 16) >= cus;
 #endif
   const int64_t n_mtiles = t16 ? (n + 15) / 16 : (n + 7) / 8;
-  int64_t total = cus;
-  if (total > groups * n_mtiles) total = groups * n_mtiles;
-  if (total < groups) total = groups;
+  const int64_t total = group_grid(cus, groups, n_mtiles);
   if (t16)
     hipLaunchKernelGGL(bc_forward_dmk_kernel<16>, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat,
                        bias, bias_dt, y);

@@ -77,12 +77,28 @@ def _rne16(v):
     return np.asarray(v, np.float32).astype(np.float16).astype(np.float64)
 
 
-def dm_forward(x, c, exact=True, single_x=False):
+def dm_forward(x, c, exact=True, single_x=False, head=None):
     """x (N, K) float32, c (nO, nI, 128): the kernel's fp32 output (no bias). exact: the
     BCFFT_ALGO_DFTX variant (a, d and Y as hi + lo); else "dft" (one RNE term each). single_x:
-    the bf16-I/O kernel of bcfft_dm8.hip, whose X is one RNE fp16 term too."""
+    the bf16-I/O kernel of bcfft_dm8.hip, whose X is one RNE fp16 term too.
+
+    head: the streamed-weight kernel of bcfft_dmk.hip (K > 4096, any nI; single_x implied).
+    Each 16-block chunk (the last zero-padded) gets the scale exponent sx - head, and the chunks
+    are aligned to the token's running reference: R = the first chunk's exponent, lowered to
+    e + head by a chunk of exponent e < R - head (whose accumulated products then scale down by
+    the same power of two). Powers of two are exact, so the result is each chunk aligned to the
+    final R."""
     n, k = x.shape
     no, ni, b = c.shape
+    if head is not None:
+        single_x = True
+        exact = False
+        pad = (-ni) % 16
+        if pad:
+            c = np.concatenate([c, np.zeros((no, pad, b), c.dtype)], axis=1)
+            x = np.concatenate([x, np.zeros((n, pad * b), x.dtype)], axis=1)
+            ni += pad
+            k += pad * b
     assert b == 128 and ni * b == k and ni % 16 == 0
     h = 64
     F = dm_table()
@@ -96,7 +112,7 @@ def dm_forward(x, c, exact=True, single_x=False):
         nsc = []
         for hh in range(halves):
             blk = xr[16 * hh:16 * hh + 16]
-            sx = _scale_exp(2.0 * np.abs(blk).max())
+            sx = _scale_exp(2.0 * np.abs(blk).max()) - (head or 0)
             s = 2.0 ** sx
             lo, hi = blk[:, :64], blk[:, 64:]
             a = ((lo + hi).astype(np.float32) * np.float32(s)).astype(np.float64)
@@ -120,6 +136,10 @@ def dm_forward(x, c, exact=True, single_x=False):
             X[16 * hh:16 * hh + 16] = (shi[..., 0] + slo[..., 0]) + 1j * (shi[..., 1] + slo[..., 1])
             nsc.append(sx - 7)
         nmin = min(nsc)
+        if head is not None:                                      # the running reference
+            nmin = nsc[0]
+            for e in nsc[1:]:
+                nmin = min(nmin, e + head)
         for hh in range(halves):                                  # exact power-of-two alignment
             X[16 * hh:16 * hh + 16] *= 2.0 ** (nmin - nsc[hh])
         # stage 2: complex MAC per bin, bin 0 as two real products with the extra 1/2

@@ -114,3 +114,26 @@ def test_dmk_full_size_and_linearity(dev):
     lhs = ops.forward((xt.float() + x2.float()).to(torch.bfloat16), spec, None, b, m, algo="dft").float()
     rhs = y.float() + ops.forward(x2, spec, None, b, m, algo="dft").float()
     assert ((lhs - rhs).norm() / rhs.norm()).item() < 1e-2
+
+
+def test_dmk_bf16_matches_numpy_model(dev):
+    """The kernel's bf16 output equals its numpy mirror (tests/dm_model.py, head=4: chunked
+    scales, headroom, running reference) rounded to bf16, except for rounding flips at bf16
+    ties; both 8-token tiles (N = 21) and the chunk-scale extremes are covered."""
+    from dm_model import dm_forward
+    k, m, b = 5120, 1024, 128                      # nI = 40: chunks of 16, 16 and 8 blocks
+    rng = np.random.default_rng(13)
+    c = (rng.standard_normal((m // b, k // b, b)) * 0.01).astype(np.float32)
+    x = rng.standard_normal((21, k)).astype(np.float32)
+    x[1, 4200:4300] *= 3e3
+    x[2, :2048] *= 3e3
+    x[3, 2048:4096] *= 10.0
+    x[9] *= 1e-4
+    xr = O.round_to(x, O.BF16)
+    y, ref = _run(dev, x, c, None, "bfloat16", "bfloat16", algo="dft")
+    g = y.float().cpu().numpy()
+    mdl = O.round_to(dm_forward(xr, O.round_to(c, O.BF16), head=4), O.BF16)
+    assert np.mean(g == mdl) > 0.97, np.mean(g == mdl)
+    assert rel_err(g, mdl) < 1e-3
+    for t in range(x.shape[0]):
+        assert rel_err(g[t], ref[t]) < 4e-3, t
