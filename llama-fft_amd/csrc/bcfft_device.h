@@ -443,8 +443,8 @@ __device__ __forceinline__ void stage_store(float* dst, uint4 v) {
 // the grid is a multiple of 8 x groups the map is XCD-aware: blocks are dealt round-robin over
 // the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch), so block b = 8 i + xcd takes group
 // i % groups and lane 8 (i / groups) + xcd. Every group's workgroup of one tile lane then sits
-// on the same XCD and the tile's x is fetched from HBM once, not once per group (PMC at
-// 4096 -> 11008, 3 groups: 196 -> 74 MB of reads). Otherwise group = b % groups.
+// on the same XCD and the tile's x is fetched from HBM once, not once per group. Otherwise
+// group = b % groups.
 struct GroupMap { int grp, lane, stride; };
 __device__ __forceinline__ GroupMap group_map(int n_groups) {
   const int b = blockIdx.x;
@@ -453,13 +453,18 @@ __device__ __forceinline__ GroupMap group_map(int n_groups) {
   const int g = b % n_groups;
   return {g, b / n_groups, ((int)gridDim.x - g + n_groups - 1) / n_groups};
 }
-// grid for group_map: one workgroup per CU, trimmed to a multiple of 8 x groups when several
-// groups share enough tiles and the trim idles at most 1/16 of the CUs (3 or 6 groups: 240 of
-// 256; 11 groups would keep only 176), never more than groups x tiles nor fewer than groups
+// grid for group_map: one workgroup per CU, never more than groups x tiles nor fewer than
+// groups. It is not trimmed to a multiple of 8 x groups. Trimming 256 CUs to 240 for 3 groups
+// cut the HBM reads at 4096 -> 11008 bf16 from 196 to 74 MB (PMC), but it did not save time:
+// these kernels are compute-bound. In one A/B session
+// (`BCFFT_XCD_TRIM`, profiles/r02_ab_xcd_map.log) config 2 was level (83-86 us either way),
+// while the fused gate/up went from 180 to 189 us and b = 64 4096 -> 11008 from 136 to 140 us.
 inline int64_t group_grid(int64_t cus, int groups, int64_t n_mtiles) {
   int64_t total = cus;
+#ifdef BCFFT_XCD_TRIM                               // analysis builds only
   const int64_t xt = cus / (8 * groups) * (8 * groups);
   if (groups > 1 && n_mtiles * groups >= cus && xt * 16 >= cus * 15) total = xt;
+#endif
   if (total > groups * n_mtiles) total = groups * n_mtiles;
   if (total < groups) total = groups;
   return total;

@@ -35,12 +35,37 @@ def t_one(k, m, b, io, algo, n=8192, iters=50):
           f"{nbytes / us / 1e3 / 8000:.3f} of 8 TB/s", flush=True)
 
 
+def t_glu(k=4096, m=11008, b=128, n=8192, iters=50):
+    """fused gate/up + SwiGLU (bcfft_forward_glu) at config 2, bf16"""
+    torch.manual_seed(1)
+    cg = (torch.randn(m // b, k // b, b) * 0.01).cuda().to(torch.bfloat16)
+    cu = (torch.randn(m // b, k // b, b) * 0.01).cuda().to(torch.bfloat16)
+    spec = ops.spectra(ops.glu_weights(cg, cu))
+    x = torch.randn(n, k, device="cuda").to(torch.bfloat16)
+    for _ in range(150):
+        ops.forward_glu(x, spec, b, m)
+    reps = []
+    for _ in range(5):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(iters):
+            ops.forward_glu(x, spec, b, m)
+        e.record()
+        torch.cuda.synchronize()
+        reps.append(s.elapsed_time(e) / iters * 1e3)
+    print(f"glu        {k}x{m} b{b} bf16 N={n}: {sorted(reps)[2]:8.1f} us", flush=True)
+
+
 if __name__ == "__main__":
     shapes = [(4096, 4096, 128, "fp32", 8192), (4096, 4096, 128, "bf16", 8192), (4096, 11008, 128, "bf16", 8192),
               (4096, 4096, 64, "fp32", 8192)]
     algos = [a for a in sys.argv[1:] if not a.startswith("--")] or ["stationary", "mfma", "valu"]
     if "--down" in sys.argv:                        # K > 4096: the streamed-weight kernel vs split-K MFMA
         shapes = [(11008, 4096, 128, "bf16", n) for n in (16, 64, 256, 1024, 1700, 8192)]
+    if "--xcd" in sys.argv:                         # shapes with several output groups (+ fused gate/up)
+        shapes = [(4096, 11008, 128, "bf16", 8192), (4096, 11008, 64, "bf16", 8192), (4096, 4096, 64, "bf16", 8192)]
+        t_glu()
     if "--down2" in sys.argv:
         shapes = [(11008, 4096, 128, "bf16", n) for n in (1700, 8192)]
     if "--smalln" in sys.argv:                      # AUTO's small-N crossover
