@@ -525,9 +525,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
 
   // Pipeline per M-tile m of 16 tokens (region r holds its chunk 0; the other region the
   // previous tile's Y units of tokens 8-15), two barriers per chunk step:
-  //   step 0   B(0); stage 3 of the previous tile's deferred token                  | B0 |
-  //            DMA x(1) into the other region, stage 1                              | Ba |
-  //            stage 2 on B(0), loading B(1) N-tile by N-tile                       | Bb |
+  //   step 0   B(0); stage 1; stage 3 of the previous tile's deferred token         | Ba |
+  //            DMA x(1) into the other region; stage 2 on B(0), loading B(1)        | Bb |
   //   step c   DMA x(c + 1) (or the next tile's chunk 0) into the other region,
   //            stage 1                                                              | Ba |
   //            stage 2 on B(c), loading B(c + 1) unless c is the last chunk         | Bb |
@@ -550,16 +549,16 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
       DSTAMP(0);
       load_b(0, 0, breg);                           // B(0): issued here, not carried across the
       load_b(0, 1, breg);                           // tile end (the accumulators are dead now)
-      stage3(other, wave, wrr[8 * LH + wave], mprev >= 0 ? mprev * TT + 8 * LH + wave : -1);
-      DSTAMP(1);
-      lds_barrier();                                // B0: the other region is free
-      DSTAMP(2);
-      dma_chunk(m, 1, other);
-      wait_vmcnt<24 + NDMA>();                      // x(0): older than B(0), 8 stores and x(1)
+      wait_vmcnt<16 + 8 * (MT - 1)>();              // x(0): older than B(0) and a half tile's stores
+      // stage 1 of this tile and the deferred stage 3 of the previous one touch different
+      // regions: one barrier for both, and the scheduler may interleave them
       stage1(region);
+      DSTAMP(1);
+      stage3(other, wave, wrr[8 * LH + wave], mprev >= 0 ? mprev * TT + 8 * LH + wave : -1);
       DSTAMP(3);
-      lds_barrier();                                // Ba
+      lds_barrier();                                // B0 + Ba: X(0) complete, the other region free
       DSTAMP(4);
+      dma_chunk(m, 1, other);
       stage2(region, breg, 1, std::true_type{});
       DSTAMP(5);
       lds_barrier();                                // Bb

@@ -14,8 +14,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from bcfft import _lib, ops  # noqa: E402
 
-NAMES = {0: "step0 top", 1: "stage3 (prev half)", 2: "B0 wait", 3: "DMA+B+stage1", 4: "Ba wait",
-         5: "stage2 (first)", 6: "Bb wait"}
+NAMES = {0: "step0 top", 1: "B(0)+stage1", 3: "stage3 (prev half)", 4: "Ba wait",
+         5: "DMA+stage2 (first)", 6: "Bb wait"}
 for c in range(1, 6):
     NAMES[7 + 3 * (c - 1)] = f"c{c}: wait+DMA+stage1"
     NAMES[8 + 3 * (c - 1)] = f"c{c}: Ba wait"
