@@ -557,7 +557,7 @@ void launch_forward_dm8(const void* x, int64_t n, int n_out, const void* spec, c
 // streamed-weight DFT kernel (bcfft_dmk.hip): b = 128, K > 4096, bf16 x and bf16 y
 bool dmk_eligible(int n_in, int b, int xdt, bool yf32);
 #ifndef BCFFT_DMK_MIN_TOKENS
-#define BCFFT_DMK_MIN_TOKENS 32      // AUTO picks the streamed-weight kernel from this many tokens
+#define BCFFT_DMK_MIN_TOKENS 1       // AUTO picks the streamed-weight kernel from this many tokens
 #endif
 void launch_forward_dmk(const void* x, int64_t n, int n_in, int n_out, const void* spec, const void* bias,
                         int bias_dt, void* y, hipStream_t s);

@@ -738,8 +738,8 @@ int bcfft_spectra(const void* c, int c_dtype, int n_out_blocks, int n_in_blocks,
 static int resolve_algo(int algo, int n_in, int block_size, int xdt = -1, bool yf32 = true, int64_t n_tokens = -1) {
   if (algo != BCFFT_ALGO_AUTO) return algo;
   if (bcfft::dm_eligible(n_in, block_size) || bcfft::dm64_eligible(n_in, block_size, xdt, yf32)) return BCFFT_ALGO_DFT;
-  // K > 4096 at b = 128 (bf16): the streamed-weight DFT kernel from BCFFT_DMK_MIN_TOKENS up; below
-  // it the split-K MFMA kernel fills the chip better
+  // K > 4096 at b = 128 (bf16): the streamed-weight DFT kernel, from one token up (it beats the
+  // split-K MFMA kernel at every measured N: 20.9 vs 23.4 us at N = 1, profiles/r02_dmk_decode_sizes.log)
   if (bcfft::dmk_eligible(n_in, block_size, xdt, yf32) && n_tokens >= BCFFT_DMK_MIN_TOKENS) return BCFFT_ALGO_DFT;
   return bcfft::stat_eligible(n_in, block_size) ? BCFFT_ALGO_STAT
                                                 : (block_size <= 128 ? BCFFT_ALGO_MFMA : BCFFT_ALGO_VALU);

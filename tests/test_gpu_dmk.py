@@ -57,9 +57,8 @@ def test_dmk_bf16_vs_oracle(dev, k, m, n, bias):
     x = rng.standard_normal((n, k)).astype(np.float32)
     y, ref = _run(dev, x, c, bv, "bfloat16", "bfloat16", algo="dft")
     _check(y, ref, "bfloat16")
-    if n >= 32:                                   # AUTO resolves to it from 32 tokens
-        ya, _ = _run(dev, x, c, bv, "bfloat16", "bfloat16", algo="auto")
-        assert torch.equal(y, ya)
+    ya, _ = _run(dev, x, c, bv, "bfloat16", "bfloat16", algo="auto")   # AUTO resolves to it
+    assert torch.equal(y, ya)
 
 
 @pytest.mark.parametrize("n", [11, 4100])
