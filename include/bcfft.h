@@ -46,7 +46,9 @@ enum bcfft_dtype { BCFFT_NONE = -1, BCFFT_F32 = 0, BCFFT_F16 = 1, BCFFT_BF16 = 2
  *  DFT:  the STAT weights, with the forward and inverse DFTs of the blocks also on the matrix
  *        cores (dense fp16 GEMMs against a 2^-7-scaled DFT table, even/odd split) instead of
  *        VALU FFTs; ~3.5e-4 relative (fp16 outputs: as DFTX). Geometry: block_size 128 with
- *        in_features 4096.
+ *        in_features 4096; block_size 64 with in_features 4096 and bf16 I/O; and block_size 128
+ *        with 4096 < in_features <= 127 * 128 and bf16 I/O, where the weight spectra are
+ *        streamed from L2 per 16-block K-chunk (the LLaMA down projection; bcfft_dmk.hip).
  *  DFTX: DFT with the per-bin products also split hi + lo before the inverse transform:
  *        ~2.8e-4 relative and linear in x to ~1e-6, ~6 % slower.
  *  AUTO: DFT where eligible, else STAT where eligible, else MFMA for block_size <= 128, else VALU. */

@@ -496,7 +496,7 @@ constexpr int STAT_OUT_BLOCKS = 32;    // output blocks per stationary group (tw
 // streamed-weight DFT kernel geometries (bcfft_dmk.hip): b = 128 with K > 4096. The same 16-B
 // header, then per output group of 32 blocks, per 16-block K-chunk, per wave (4), per bin of
 // the wave (16), per N-tile (2), per lane: the fp16 B fragment the lane loads for that chunk
-__host__ __device__ inline bool dmk_geometry(int n_in, int b) { return b == 128 && n_in > 32; }
+__host__ __device__ inline bool dmk_geometry(int n_in, int b) { return b == 128 && n_in > 32 && n_in <= 127; }
 constexpr int DMK_FRAGS_PER_CHUNK = 4 * 16 * 2;   // waves x bins per wave x N-tiles
 __host__ __device__ inline SpecLayout spec_layout(int n_out, int n_in, int b) {
   SpecLayout s;
