@@ -7,30 +7,33 @@
 // is where the weights live. An output group's fp16 spectra at K = 11008 are 704 KiB: more than
 // the register file and the LDS together, so they cannot stay resident as in bcfft_dm8.hip.
 // Instead the K axis is cut into 16-block chunks and each chunk's B fragments are streamed from
-// L2 into VGPRs once per M-tile of 16 tokens, while the per-bin products accumulate in the
+// L2 into VGPRs once per M-tile (TT = 8 or 16 tokens), while the per-bin products accumulate in
 // registers over all chunks.
 //
 //  * Workgroup: 8 waves (two per SIMD), persistent, one per CU. Wave w owns the 8 bins
-//    8w .. 8w + 7 and keeps Y of the tile's 16 tokens for them: 8 bins x 2 M-tiles (8 tokens
-//    x re/im) x 2 N-tiles (16 output blocks) of fp32 accumulators = 128 registers.
-//  * Per chunk step: wave w streams x of tokens 2w, 2w + 1 (16 blocks, 4 KiB of bf16 each)
-//    into LDS one step ahead (LDS-DMA), loads its 16 B fragments of the chunk (64 VGPRs,
-//    buffer loads) and runs stage 1 of its tokens; barrier; stage 2 of all 16 tokens on its
-//    bins; barrier. Each B fragment serves 16 tokens: the L2 -> CU stream of weights is
-//    48 KiB per token.
-//  * Tile end: Y of tokens 0-7 as fp16 units into the last chunk's region, stage 3 of token w
-//    (y staged in LDS, 1 KiB stores); then Y of tokens 8-15, whose stage 3 runs at the start
-//    of the next tile.
-//  * Numerics: per-(token, chunk) power-of-two scales from stage 1. Stage 2 aligns each chunk
-//    to the token's loudest chunk so far: A rows are multiplied by 2^-d (exact, no fp16
-//    overflow), and when a later chunk is louder the token's accumulator rows are scaled down
-//    once. a, d, X and Y are one RNE fp16 term each, C and the table one term each, fp32
-//    accumulation: the bf16 kernel's numerics (tests/dm_model.py, single_x).
+//    8w .. 8w + 7 and keeps Y of the tile's TT tokens for them: 8 bins x TT/8 M-tiles (8 tokens
+//    x re/im) x 2 N-tiles (16 output blocks) of fp32 accumulators (64 or 128 registers).
+//  * Per chunk step: wave w streams x of its TT/8 tokens (16 blocks, 4 KiB of bf16 each) into
+//    LDS one step ahead (LDS-DMA) and runs stage 1 of them; barrier; stage 2 of all TT tokens on
+//    its bins against the chunk's 16 B fragments (64 VGPRs), loading the next chunk's fragments
+//    bin by bin as each bin is done; barrier. Each fragment serves TT tokens: the L2 -> CU weight
+//    stream is 96 or 48 KiB per token.
+//  * Tile end: Y as fp16 units into the last chunk's region, 8 tokens at a time, with stage 3 of
+//    token w (y staged in LDS, 1 KiB stores); the last 8 tokens' stage 3 runs at the start of
+//    the next tile, beside its first stage 1.
+//  * The launcher takes 16-token tiles once every CU gets one, else 8 (a tile is a serial chain
+//    of chunk steps, so small N wants more, shorter tiles).
+//  * Numerics: per-(token, chunk) power-of-two scales from stage 1, which keeps |X| < 2^(14 -
+//    HEAD). Stage 2 aligns each chunk to the token's reference exponent (the first chunk's,
+//    lowered when a chunk is more than 2^HEAD louder): A rows are multiplied by 2^-d, d >= -HEAD
+//    (exact, below fp16's max), and a lowered reference scales the token's accumulator rows
+//    down once. a, d, X and Y are one RNE fp16 term each, C and the table one term each, fp32
+//    accumulation (tests/dm_model.py, head = 4, mirrors it).
 //
-// LDS (149,632 B): two regions of 16 x-chunk slots of 4,160 B (8 Y / y-staging slots of
-// 8,256 B at the tile end), the DFT table, the scales. Slot strides are
-// 64 B off the 256-B bank period, as in bcfft_dm8.hip, so the stage-2 reads of eight tokens at
-// once are conflict-free; all in-slot offsets are bcfft_dm8.hip's.
+// LDS (TT = 16: 149,632 B; TT = 8: 148,608 B): two regions of x-chunk slots of 4,160 B, each also
+// holding 8 Y / y-staging slots of 8,256 B at the tile end, the DFT table, the scales. Slot
+// strides are 64 B off the 256-B bank period, as in bcfft_dm8.hip, so the stage-2 reads of eight
+// tokens at once are conflict-free; all in-slot offsets are bcfft_dm8.hip's.
 #include "bcfft_device.h"
 #include "bcfft_dm_table.h"
 #include "bcfft_dm_common.h"
@@ -163,7 +166,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
 #pragma unroll
     for (int fb = 0; fb < BPW; ++fb) load_b1(brs, vo, fb, nt, breg);
   };
-  // wait until at most N younger VMEM operations are outstanding: N. tile's fragments landed
+  // wait until at most N VMEM operations younger than N-tile nt's fragments are outstanding:
+  // those fragments have then landed
   auto wait_b = [&](auto n_tag, int nt, u32x4 (&breg)[BPW][NT]) {
     constexpr int N = decltype(n_tag)::value;
     static_assert(N >= 0 && N < 64, "vmcnt");
