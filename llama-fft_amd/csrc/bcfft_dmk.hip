@@ -657,12 +657,17 @@ void launch_forward_dmk(const void* x, int64_t n, int n_in, int n_out, const voi
   const SpecLayout sl = spec_layout(n_out, n_in, 128);
   const int64_t cus = device_cu_count();
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
-  // 16-token tiles halve the weight stream per token; 8-token tiles finish a tile in about half
-  // the time, so they win while 16-token tiles would leave CUs idle
+  // A tile is a serial chain of chunk steps: the launch takes about (tiles per CU, rounded up)
+  // x the tile time, ~21.7 us for 8 tokens and ~39.7 us for 16 at nI = 86 (16-token tiles
+  // halve the weight stream per token). The smaller makespan wins; this model picks the faster
+  // size at every measured N (profiles/r02_ab_dmk_tile_switch.log: 16 at N = 3000 and 4096, 8
+  // at 5000 and 6144, 16 at 8192, 8 at 1700).
 #ifdef BCFFT_DMK_TILE
   const bool t16 = BCFFT_DMK_TILE == 16;           // analysis builds: force a tile size
 #else
-  const bool t16 = groups * ((n + 15) / 16) >= cus;
+  const int64_t waves8 = (groups * ((n + 7) / 8) + cus - 1) / cus;
+  const int64_t waves16 = (groups * ((n + 15) / 16) + cus - 1) / cus;
+  const bool t16 = waves16 * 40 < waves8 * 22;
 #endif
   const int64_t n_mtiles = t16 ? (n + 15) / 16 : (n + 7) / 8;
   const int64_t total = group_grid(cus, groups, n_mtiles);

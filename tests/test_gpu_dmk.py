@@ -61,11 +61,12 @@ def test_dmk_bf16_vs_oracle(dev, k, m, n, bias):
     assert torch.equal(y, ya)
 
 
-@pytest.mark.parametrize("n", [11, 4100])
+@pytest.mark.parametrize("n", [11, 4090])
 def test_dmk_per_token_chunk_scales(dev, n):
     """Chunks of one token at very different magnitudes, in both orders (a later louder chunk
     scales the accumulated rows down), zero and tiny tokens, a single massive channel. n = 11
-    runs 8-token tiles; n = 4100 fills every CU with 16-token tiles (the last one ragged)."""
+    runs 8-token tiles; n = 4090 runs one 16-token tile per CU (the launcher's makespan rule;
+    the last tile ragged)."""
     from bcfft import ops
     k, m, b = 11008, 4096, 128
     rng = np.random.default_rng(5)
