@@ -2,14 +2,20 @@
 """Benchmark of the MI355X block-circulant (BC) linear forward — BASELINE.json's metric.
 
 Workload (north star / metric): one BlockCirculantLinear forward, 4096 -> 4096, b = 128,
-N = batch*seq = 8192 tokens per GPU, fp32 I/O (the reference's fp32 path), weight spectra
-precomputed outside the timed region (the reference's cache_cfft=1 perf convention,
-bench_all_in_one.py:484). A "step" = one forward over the rank's 8192-token shard.
+N = batch*seq = 8192 tokens, fp32 I/O (the reference's fp32 path), weight spectra precomputed
+outside the timed region (the reference's cache_cfft=1 perf convention,
+bench_all_in_one.py:484). A "step" = one forward over the rank's token shard.
 
-Multi-GPU: one process per GPU (torch.distributed.run); tokens are sharded, each rank runs
-its own 8192-token shard (weak scaling) with no collective in the data path. With
---allgather the single RCCL all-gather of the output shards (north star) is timed in a
-second loop and reported as `with_allgather`.
+Multi-GPU: one process per GPU. `--gpus N` without a torch.distributed
+environment re-launches this script under `torch.distributed.run` with N ranks before any GPU
+call; with one (the driver's launch) WORLD_SIZE must equal --gpus. `--partition global` (the
+default, §8e): the GLOBAL batch*seq = 8192 tokens are split into contiguous shards of
+ceil(8192 / N) rows (1024 per rank at N = 8) and every rank runs its shard with no collective in
+the data path ("scaling": "strong"); `value` = 8192 x M / the slowest rank's time.
+`--partition per-rank` keeps 8192 tokens on every rank (weak scaling). With --allgather the
+single RCCL all-gather of the output shards (north star) is timed in a second loop: forward +
+all_gather_into_tensor, reported as `with_allgather` (gather-inclusive throughput) beside the
+sharded-compute `value`.
 
 Prints ONE JSON line on rank 0. `roofline.achieved` = algorithmic bytes per launch
 (N*K*s_x + N*M*s_y + nO*nI*(b/2+1)*8 [+ M*s_bias]) / the kernel's average
@@ -47,8 +53,11 @@ def algo_bytes(n, k, m, b, io, bias):
 
 def resolved_kernel(algo, k, b, io="fp32"):
     """(algorithm, kernel symbol, MAC arithmetic) that BCFFT_ALGO=algo runs for this geometry and
-    I/O dtype; mirrors bcfft_forward_algo's AUTO rule (csrc/bcfft_kernels.hip)."""
+    I/O dtype (the output has the I/O dtype); mirrors bcfft_forward_algo's AUTO rule
+    (resolve_algo in csrc/bcfft_kernels.hip): at b = 128, K = 4096 fp32 outputs take dftx."""
     n_in = k // b
+    if algo == "auto" and b == 128 and n_in == 32 and io == "fp32":
+        algo = "dftx"
     stat_ok = (b == 128 and n_in == 32) or (b == 64 and n_in in (32, 64))
     dft_ok = b == 128 and n_in == 32
     if io == "bf16" and algo in ("dft", "auto") and b == 64 and n_in == 64:
@@ -93,42 +102,111 @@ def make_layer(k, m, b, io, bias, dev, seed=1):
     return layer.to(dev).to(DT[io]).eval()
 
 
-def settle(layer, x, ms):
-    """Run the forward back to back for at least `ms` milliseconds of wall time (untimed)."""
+def settle(fn, ms, dev):
+    """Run fn back to back for at least `ms` milliseconds of wall time (untimed)."""
     t0 = time.perf_counter()
     with torch.inference_mode():
         while (time.perf_counter() - t0) * 1e3 < ms:
             for _ in range(20):
-                layer(x)
-            torch.cuda.synchronize()
+                fn()
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
 
 
-def time_layer(layer, x, steps, warmup, barrier=None):
-    """Returns (wall ms per step over the bracketed region, mean kernel ms per launch from HIP
-    events). One event pair brackets all K back-to-back launches on the launch stream: a pair
-    around EACH launch adds its own marker latency (~6 us per step measured on MI355X, see
-    tools/event_timing.py), while K launches back to back give the launch duration plus the
-    inter-kernel gap, within ~2-3 % of rocprofv3's per-kernel average."""
-    stream = torch.cuda.current_stream()
+def time_fn(fn, steps, warmup, barrier=None, dev=None):
+    """Returns (wall ms per step over the bracketed region, mean ms per launch). On a GPU the
+    second figure comes from ONE HIP-event pair around the K back-to-back launches on the launch
+    stream: a pair around EACH launch adds its own marker latency (~6 us per step measured on
+    MI355X, see tools/event_timing.py), while K launches back to back give the launch duration
+    plus the inter-kernel gap, within ~2-3 % of rocprofv3's per-kernel average. On the CPU (the
+    gloo test of the distributed path) both are the wall time."""
+    cuda = dev is not None and dev.type == "cuda"
     with torch.inference_mode():
-        layer._spectra(layer.c)                                # spectra outside timing
         for _ in range(warmup):
-            layer(x)
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            fn()
+        if cuda:
+            stream = torch.cuda.current_stream()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         if barrier:
             barrier()
-        torch.cuda.synchronize()
+        if cuda:
+            torch.cuda.synchronize()
         t0 = time.perf_counter()
-        s.record(stream)
+        if cuda:
+            s.record(stream)
         for _ in range(steps):
-            layer(x)
-        e.record(stream)
-        torch.cuda.synchronize()
+            fn()
+        if cuda:
+            e.record(stream)
+            torch.cuda.synchronize()
         if barrier:
             barrier()
         wall = (time.perf_counter() - t0) * 1e3 / steps
-    kern = s.elapsed_time(e) / steps
+    kern = s.elapsed_time(e) / steps if cuda else wall
     return wall, kern
+
+
+def time_layer(layer, x, steps, warmup, barrier=None):
+    """time_fn of one BC layer on x, spectra computed outside the timed region."""
+    with torch.inference_mode():
+        layer._spectra(layer.c)
+    return time_fn(lambda: layer(x), steps, warmup, barrier, x.device)
+
+
+def reduce_max(vals, dev, world):
+    """Elementwise max over ranks (the slowest rank sets every timed figure)."""
+    t = torch.tensor([float(v) for v in vals], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.cpu()]
+
+
+def partition(n, world, rank, mode):
+    """(tokens this rank runs, its row range in the global batch, global tokens). 'global': the
+    global n tokens in contiguous ceil(n / world) shards; 'per-rank': n each."""
+    if mode == "global":
+        from bcfft.shard import shard_bounds
+        lo, hi = shard_bounds(n, world, rank)
+        return hi - lo, (lo, hi), n
+    return n, (rank * n, (rank + 1) * n), n * world
+
+
+def run_partitioned(fwd, x_local, n_total, steps, warmup, world, barrier, dev, settle_ms=0.0,
+                    allgather=True, repeats=5):
+    """The timed core every rank runs (GPU ranks over RCCL, and the gloo test on CPU stubs):
+    settle, then W warmup + K timed steps of fwd on the rank's shard between barriers, the max
+    over ranks; `repeats` more K-step windows; with N > 1 and allgather, forward + the single
+    all-gather of the y shards (bcfft.shard.gather_rows) timed the same way. Returns
+    {wall, kern, reps (sorted), gather_wall or None}."""
+    from bcfft.shard import gather_rows
+    step = lambda: fwd(x_local)  # noqa: E731
+    settle(step, settle_ms, dev)
+    wall, kern = reduce_max(time_fn(step, steps, warmup, barrier, dev), dev, world)
+    reps = sorted(reduce_max([time_fn(step, steps, 2, barrier, dev)[1] for _ in range(repeats)], dev, world))
+    gather = None
+    if world > 1 and allgather:
+        g = time_fn(lambda: gather_rows(fwd(x_local), n_total), steps, 3, barrier, dev)[0]
+        gather = reduce_max([g], dev, world)[0]
+    return {"wall": wall, "kern": kern, "reps": reps, "gather_wall": gather}
+
+
+def spawn_cmd(gpus, argv, port):
+    """The torch.distributed.run command that re-launches this script with one rank per GPU."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def spawn_ranks(gpus, argv):
+    """`bench.py --gpus N` outside torch.distributed: start N fresh rank processes (nothing here
+    has touched the GPU yet) and return their launcher's exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(spawn_cmd(gpus, argv, port), env=env)
 
 
 def time_spectra(layer, iters=20):
@@ -174,33 +252,83 @@ def time_glu(dev, steps, k=4096, m=11008, b=128, n=8192, io="bf16"):
         fused_stat = run(lambda: ops.forward_glu(x, sgu, b, m, algo="stationary"))
         unfused = run(lambda: torch.nn.functional.silu(ops.forward(x, sg, None, b, m)) * ops.forward(x, su, None, b, m))
     nbytes = n * k * SZ[io] + n * m * SZ[io] + 2 * (m // b) * (k // b) * (b // 2 + 1) * 8
-    engine = "dft-glu" if resolved_kernel("auto", k, b)[0] == "dft" else "stationary-glu"
+    engine = "dft-glu" if resolved_kernel("auto", k, b, io)[0] in ("dft", "dftx") else "stationary-glu"
     return {"workload": f"gate/up {k}->{m} b={b} N={n} {io}-io + SwiGLU", "engine": engine,
             "ms": round(fused, 4), "stationary_glu_ms": round(fused_stat, 4), "unfused_ms": round(unfused, 4),
             "GB_s": round(nbytes / (fused * 1e-3) / 1e9, 1),
             "frac": round(nbytes / (fused * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
-def load_traffic(tag, kernel):
-    """Per-launch HBM bytes of this kernel on this workload from the newest
-    profiles/pmc_traffic_*.json that measured that pair (None if none did)."""
+def load_traffic(tag, kernel, algo=None):
+    """Per-launch HBM bytes of this kernel and engine on this workload from the newest
+    profiles/pmc_traffic_*.json that measured that triple (None if none did; tools/pmc_traffic.py
+    writes them from rocprofv3 PMC passes: FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic_*.json")))
     for f in reversed(files):
         try:
             d = json.load(open(f))
         except Exception:
             continue
-        if tag in d and d[tag].get("kernel") == kernel:
-            return d[tag].get("hbm_bytes_per_launch")
+        e = d.get(tag)
+        if e and e.get("kernel") == kernel and (algo is None or e.get("algo", algo) == algo):
+            return e.get("hbm_bytes_per_launch")
     return None
+
+
+def run_variants(dev, algo, steps):
+    """SURVEY.md §8d beside the headline: config 1 (4096², b=64, N=128 fp32), config 2
+    (4096->11008 b=128 bf16), the north star in bf16 and on the other engines, the config-4 sweep
+    b x shape (bf16), and config 2's fused gate/up + SwiGLU."""
+    vlist = [(4096, 4096, 64, "fp32", 128, "auto"),
+             (4096, 4096, 128, "bf16", 8192, "auto"),
+             (4096, 4096, 128, "fp32", 8192, "dft"),
+             (4096, 4096, 128, "fp32", 8192, "stationary"),
+             (4096, 4096, 128, "bf16", 8192, "stationary"),
+             (4096, 4096, 128, "fp32", 8192, "mfma"),
+             (4096, 4096, 128, "fp32", 8192, "valu")]
+    for vb in (64, 128, 256):
+        for (vk, vm) in ((4096, 4096), (4096, 11008), (11008, 4096)):
+            if not (vb == 128 and (vk, vm) == (4096, 4096)):
+                vlist.append((vk, vm, vb, "bf16", 8192, "auto"))
+    variants = []
+    for (vk, vm, vb, vio, vn, va) in vlist:
+        os.environ["BCFFT_ALGO"] = va
+        vl = make_layer(vk, vm, vb, vio, False, dev)
+        vx = torch.randn(vn, vk, device=dev).to(DT[vio])
+        vw, vkern = time_layer(vl, vx, max(10, steps // 2), 5)
+        os.environ["BCFFT_ALGO"] = algo
+        vbytes = algo_bytes(vn, vk, vm, vb, vio, False)
+        variants.append({"workload": f"{vk}->{vm} b={vb} N={vn} {vio}-io algo={va}",
+                         "engine": resolved_kernel(va, vk, vb, vio)[1].replace("bc_forward_", "").replace("_kernel", ""),
+                         "ms": round(vkern, 4),
+                         "GTok_elem_s": round(vn * vm / (vkern * 1e-3) / 1e9, 3),
+                         "GB_s": round(vbytes / (vkern * 1e-3) / 1e9, 1),
+                         "frac": round(vbytes / (vkern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+        del vl, vx
+    variants.append(time_glu(dev, max(10, steps // 2)))
+    return variants
+
+
+def host_cores():
+    """Host cores this process may run on: the affinity mask, capped by a cgroup CPU quota where
+    one is set (a GPU box's share of a many-core host shows all of the host's CPUs in
+    os.cpu_count())."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def cpu_baseline(k, m, b, io, bias, budget_s):
     """Oracle's torch-CPU restatement of the cached forward (bench_all_in_one.py:179-231),
-    fp32, on a bounded token sample; GTok-elem/s."""
+    fp32, on a bounded token sample, on all the host cores this process may use; GTok-elem/s."""
     sys.path.insert(0, ROOT)
     from oracle.bc_oracle import torch_cpu_forward_cached
-    threads = int(os.environ.get("BENCH_CPU_THREADS", min(os.cpu_count() or 1, 16)))
+    threads = int(os.environ.get("BENCH_CPU_THREADS", host_cores()))
     torch.set_num_threads(threads)
     n = 1024
     g = torch.Generator().manual_seed(0)
@@ -222,12 +350,16 @@ def cpu_baseline(k, m, b, io, bias, budget_s):
                       f"irfft, cached spectra), {el:.1f} s on {threads} threads"}
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--tokens", type=int, default=8192, help="tokens per rank (batch*seq)")
+    ap.add_argument("--tokens", type=int, default=8192,
+                    help="batch*seq: global tokens (--partition global) or tokens per rank (per-rank)")
+    ap.add_argument("--partition", default="global", choices=("global", "per-rank"),
+                    help="global: shard the global tokens over the ranks (SURVEY.md §8e, strong scaling); "
+                         "per-rank: every rank runs --tokens (weak scaling)")
     ap.add_argument("--in-features", type=int, default=4096)
     ap.add_argument("--out-features", type=int, default=4096)
     ap.add_argument("--block-size", type=int, default=128)
@@ -238,112 +370,103 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU baseline work")
     ap.add_argument("--settle-ms", type=float, default=300.0,
                     help="untimed clock-settle phase of the hot path on every rank before the W warmup steps")
-    args = ap.parse_args()
+    ap.add_argument("--stub", default="",
+                    help="tests only: module:function returning a CPU forward(k, m, b) for a gloo run of the "
+                         "launcher and the distributed timing core without a GPU")
+    return ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:          # before anything touches the GPU
+        sys.exit(spawn_ranks(args.gpus, argv))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; run one rank per GPU "
+                         f"(torch.distributed.run --nproc-per-node {args.gpus}) or drop WORLD_SIZE")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    stub = None
+    if args.stub:
+        import importlib
+        mod, fn = args.stub.split(":")
+        stub = getattr(importlib.import_module(mod), fn)
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-        barrier = lambda: dist.barrier(device_ids=[local])  # noqa: E731
+        barrier = (lambda: dist.barrier()) if stub else (lambda: dist.barrier(device_ids=[local]))
     else:
         barrier = None
 
-    n, k, m, b, io = args.tokens, args.in_features, args.out_features, args.block_size, args.io
+    k, m, b, io = args.in_features, args.out_features, args.block_size, args.io
+    n_local, (lo, hi), n_total = partition(args.tokens, world, rank, args.partition)
     algo = os.environ.setdefault("BCFFT_ALGO", "auto")
-    layer = make_layer(k, m, b, io, bool(args.bias), dev)
-    torch.manual_seed(1000 + rank)                           # x ~ N(0,1) per rank shard
-    x = torch.randn(n, k, device=dev).to(DT[io])
+    if stub:
+        fwd = stub(k, m, b)
+        layer = None
+    else:
+        layer = make_layer(k, m, b, io, bool(args.bias), dev)
+        fwd = layer
+    if args.partition == "global":                   # one global batch, the rank's contiguous rows
+        torch.manual_seed(1000)
+        x = torch.randn(n_total, k, device=dev)[lo:hi].to(DT[io]).contiguous()
+    else:
+        torch.manual_seed(1000 + rank)
+        x = torch.randn(n_local, k, device=dev).to(DT[io])
 
     # the variant sweep (rank 0, N=1) runs first: real work, timed per variant
     variants = []
-    if args.variants and rank == 0 and world == 1:
-        # config 1 (4096², b=64, N=128 fp32), config 2 (4096->11008 b=128 bf16),
-        # the north star in bf16 and on the other engines, and the config-4 sweep b x shape (bf16)
-        vlist = [(4096, 4096, 64, "fp32", 128, "auto"),
-                 (4096, 4096, 128, "bf16", 8192, "auto"),
-                 (4096, 4096, 128, "fp32", 8192, "dftx"),
-                 (4096, 4096, 128, "fp32", 8192, "stationary"),
-                 (4096, 4096, 128, "bf16", 8192, "stationary"),
-                 (4096, 4096, 128, "fp32", 8192, "mfma"),
-                 (4096, 4096, 128, "fp32", 8192, "valu")]
-        for vb in (64, 128, 256):
-            for (vk, vm) in ((4096, 4096), (4096, 11008), (11008, 4096)):
-                if not (vb == 128 and (vk, vm) == (4096, 4096)):
-                    vlist.append((vk, vm, vb, "bf16", 8192, "auto"))
-        for (vk, vm, vb, vio, vn, va) in vlist:
-            os.environ["BCFFT_ALGO"] = va
-            vl = make_layer(vk, vm, vb, vio, False, dev)
-            vx = torch.randn(vn, vk, device=dev).to(DT[vio])
-            vw, vkern = time_layer(vl, vx, max(10, args.steps // 2), 5)
-            os.environ["BCFFT_ALGO"] = algo
-            vbytes = algo_bytes(vn, vk, vm, vb, vio, False)
-            variants.append({"workload": f"{vk}->{vm} b={vb} N={vn} {vio}-io algo={va}",
-                             "engine": resolved_kernel(va, vk, vb, vio)[1].replace("bc_forward_", "").replace("_kernel", ""),
-                             "ms": round(vkern, 4),
-                             "GTok_elem_s": round(vn * vm / (vkern * 1e-3) / 1e9, 3),
-                             "GB_s": round(vbytes / (vkern * 1e-3) / 1e9, 1),
-                             "frac": round(vbytes / (vkern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
-            del vl, vx
-        variants.append(time_glu(dev, max(10, args.steps // 2)))
+    if args.variants and rank == 0 and world == 1 and not stub:
+        variants = run_variants(dev, algo, args.steps)
     # Clock settle, untimed, on every rank: the same forward back to back for --settle-ms of wall
     # time. Right after a cold start the first launches run ~15 % slow while the clock ramps
     # (measured: 60 us vs 51.5 us per launch, 50 warmup steps and no other GPU work before). N > 1
     # ranks skip the variant sweep, so without this their windows would time the ramp. The W
     # warmup steps and the K timed steps that follow are exactly the contract's.
-    settle(layer, x, args.settle_ms)
-    wall, kern = time_layer(layer, x, args.steps, args.warmup, barrier)
-    t = torch.tensor([wall, kern], device=dev, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall, kern = float(t[0]), float(t[1])
-
-    # SURVEY.md §8d extras beside the contract's single K-step region: 5 more repeats of K steps
-    # (median and spread of the per-launch kernel time) and the spectra precompute time
-    reps = []
-    for _ in range(5):
-        reps.append(time_layer(layer, x, args.steps, 2, barrier)[1])
-    reps_t = torch.tensor(reps, device=dev, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(reps_t, op=dist.ReduceOp.MAX)
-    reps = sorted(float(v) for v in reps_t)
-    spectra_ms = time_spectra(layer)
-
-    nbytes = algo_bytes(n, k, m, b, io, bool(args.bias))
-    gbs = nbytes / (kern * 1e-3) / 1e9
-    total_elems = n * m * world
-    value = total_elems / (wall * 1e-3) / 1e9
-
-    gather = None
-    if world > 1 and args.allgather:
-        from bcfft.shard import gather_rows
+    if layer is not None:
         with torch.inference_mode():
-            for _ in range(3):
-                gather_rows(layer(x), world * n)
-            barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(args.steps):
-                gather_rows(layer(x), world * n)
-            torch.cuda.synchronize()
-            barrier()
-            g_ms = (time.perf_counter() - t0) * 1e3 / args.steps
-        tg = torch.tensor([g_ms], device=dev, dtype=torch.float64)
-        dist.all_reduce(tg, op=dist.ReduceOp.MAX)
-        gather = {"ms_per_step": round(float(tg[0]), 4),
-                  "value": round(total_elems / (float(tg[0]) * 1e-3) / 1e9, 3),
-                  "note": "forward + RCCL all_gather_into_tensor of all y shards to every rank"}
+            layer._spectra(layer.c)                   # spectra outside the timed region
+    r = run_partitioned(fwd, x, n_total, args.steps, args.warmup, world, barrier, dev,
+                        settle_ms=0.0 if stub else args.settle_ms, allgather=bool(args.allgather))
+    wall, kern, reps = r["wall"], r["kern"], r["reps"]
+    value = n_total * m / (wall * 1e-3) / 1e9
+    nbytes = algo_bytes(n_local, k, m, b, io, bool(args.bias))
+    gather = None
+    if r["gather_wall"] is not None:
+        gather = {"ms_per_step": round(r["gather_wall"], 4),
+                  "value": round(n_total * m / (r["gather_wall"] * 1e-3) / 1e9, 3),
+                  "note": "gather-inclusive: forward of the rank's shard + the single RCCL "
+                          "all_gather_into_tensor of all y shards to every rank (slowest rank)"}
 
-
-    tag = f"{k}x{m}_b{b}_n{n}_{io}"
-    kname = resolved_kernel(algo, k, b, io if not args.bias else "fp32")
+    spectra_ms = time_spectra(layer) if layer is not None else None
+    tag = f"{k}x{m}_b{b}_n{n_local}_{io}"
+    kname = resolved_kernel(algo, k, b, io)
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_budget > 0:
+    if rank == 0 and world == 1 and args.cpu_budget > 0 and not stub:
         cpu = cpu_baseline(k, m, b, io, bool(args.bias), args.cpu_budget)
 
     if rank == 0:
+        roofline = None
+        if not stub:
+            gbs = nbytes / (kern * 1e-3) / 1e9
+            roofline = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                        "traffic": load_traffic(tag, kname[1], kname[0]),
+                        "kernel": kname[1], "kernel_ms": round(kern, 5),
+                        "algorithmic_bytes_per_launch": nbytes,
+                        "fp32_tflops": round(algo_flops(n_local, k, m, b) / (kern * 1e-3) / 1e12, 2),
+                        "fp32_valu_peak_tflops": FP32_VALU_TFLOPS,
+                        "kernel_ms_repeats": {"n": len(reps), "steps_each": args.steps,
+                                              "median": round(reps[len(reps) // 2], 5),
+                                              "min": round(reps[0], 5), "max": round(reps[-1], 5)}}
         line = {
             "metric": METRIC,
             "value": round(value, 4),
@@ -353,29 +476,24 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(wall, 5),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.partition == "global" else "weak",
             "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (x~N(0,1) seed 1000+rank, c~0.01 N(0,1) seed 1)",
-            "config": {"workload": f"BlockCirculantLinear.forward {k}->{m} b={b}, {n} tokens/rank, "
-                                   f"{io} I/O, spectra cached",
+            "dtype": "f32" if io == "fp32" else io,
+            "data": (f"synthetic (x~N(0,1) seed {1000 if args.partition == 'global' else '1000+rank'}, "
+                     "c~0.01 N(0,1) seed 1)"),
+            "config": {"workload": f"BlockCirculantLinear.forward {k}->{m} b={b}, {n_total} tokens "
+                                   f"({args.partition} partition: {n_local} per rank), {io} I/O, spectra cached",
                        "in_features": k, "out_features": m, "block_size": b,
-                       "tokens_per_rank": n, "global_tokens": n * world, "io_dtype": io,
-                       "bias": bool(args.bias), "parallelism": f"token-shard x{world}",
+                       "tokens_per_rank": n_local, "global_tokens": n_total, "io_dtype": io,
+                       "bias": bool(args.bias), "partition": args.partition,
+                       "parallelism": f"token-shard x{world}",
                        "algo": algo, "algo_resolved": kname[0], "mac": kname[2]},
-            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
-                         "traffic": load_traffic(tag, kname[1]),
-                         "kernel": kname[1], "kernel_ms": round(kern, 5),
-                         "algorithmic_bytes_per_launch": nbytes,
-                         "fp32_tflops": round(algo_flops(n, k, m, b) / (kern * 1e-3) / 1e12, 2),
-                         "fp32_valu_peak_tflops": FP32_VALU_TFLOPS,
-                         "kernel_ms_repeats": {"n": len(reps), "steps_each": args.steps,
-                                               "median": round(reps[len(reps) // 2], 5),
-                                               "min": round(reps[0], 5), "max": round(reps[-1], 5)}},
-            "spectra_precompute_ms": round(spectra_ms, 4),
+            "roofline": roofline,
+            "spectra_precompute_ms": None if spectra_ms is None else round(spectra_ms, 4),
             "cpu_baseline": cpu,
         }
+        if stub:
+            line["stub"] = args.stub
         if gather:
             line["with_allgather"] = gather
         if variants:

@@ -51,7 +51,10 @@ enum bcfft_dtype { BCFFT_NONE = -1, BCFFT_F32 = 0, BCFFT_F16 = 1, BCFFT_BF16 = 2
  *        streamed from L2 per 16-block K-chunk (the LLaMA down projection; bcfft_dmk.hip).
  *  DFTX: DFT with the per-bin products also split hi + lo before the inverse transform:
  *        ~2.8e-4 relative and linear in x to ~1e-6, ~6 % slower.
- *  AUTO: DFT where eligible, else STAT where eligible, else MFMA for block_size <= 128, else VALU. */
+ *  AUTO: at block_size 128 with in_features 4096, DFTX for fp32 outputs (linear in x, which the
+ *        fp32 backward's dx relies on) and DFT for 16-bit outputs (whose own rounding dominates);
+ *        DFT on its other geometries; else STAT where eligible, else MFMA for block_size <= 128,
+ *        else VALU. */
 enum bcfft_algo { BCFFT_ALGO_AUTO = 0, BCFFT_ALGO_MFMA = 1, BCFFT_ALGO_VALU = 2, BCFFT_ALGO_STAT = 3,
                   BCFFT_ALGO_DFT = 4, BCFFT_ALGO_DFTX = 5 };
 
@@ -73,6 +76,10 @@ const char* bcfft_status_string(int status);
 
 /* Text of the last HIP error seen by this thread (empty if none). */
 const char* bcfft_last_hip_error(void);
+
+/* Why the last bcfft_forward* call of this thread returned BCFFT_ERR_BLOCK: the engine that was
+ * asked for and the geometry / dtypes it does not serve (empty if the call was not refused). */
+const char* bcfft_last_error_detail(void);
 
 /* Bytes of the spectra buffer of an operator with (n_out_blocks x n_in_blocks) b x b
  * circulant blocks: packed fp32 bins (n_out*n_in*b/2 complex64), a b-entry twiddle table,
@@ -122,6 +129,12 @@ int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_feat
  * epilogue: bit-reproducible, and identical per output block for q/k/v-style concatenations. */
 int64_t bcfft_forward_workspace_bytes(int64_t n_tokens, int in_features, int out_features, int block_size,
                                       int algo);
+
+/* The same for known I/O dtypes (y_dtype = promote(x_dtype, bias_dtype)): AUTO then resolves
+ * exactly as bcfft_forward_ws will, so geometries that run a DFT engine for these dtypes (e.g. the
+ * bf16 down projection on the streamed-weight kernel) report 0. < 0 for invalid arguments. */
+int64_t bcfft_forward_workspace_bytes_io(int64_t n_tokens, int in_features, int out_features, int block_size,
+                                         int algo, int x_dtype, int y_dtype);
 
 /* bcfft_forward_algo with a caller-owned device workspace (16-B aligned), used when
  * workspace_bytes >= bcfft_forward_workspace_bytes(...); NULL / too small runs unsplit. */

@@ -28,6 +28,7 @@ _SIGNATURES = {
     "bcfft_abi_version": (ctypes.c_int, []),
     "bcfft_status_string": (ctypes.c_char_p, [ctypes.c_int]),
     "bcfft_last_hip_error": (ctypes.c_char_p, []),
+    "bcfft_last_error_detail": (ctypes.c_char_p, []),
     "bcfft_spectra_bytes": (ctypes.c_int64, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "bcfft_spectra": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
@@ -40,6 +41,8 @@ _SIGNATURES = {
                                           ctypes.c_void_p]),
     "bcfft_forward_workspace_bytes": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                        ctypes.c_int]),
+    "bcfft_forward_workspace_bytes_io": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                          ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "bcfft_forward_ws": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
                                         ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
@@ -91,8 +94,9 @@ def check(status: int, what: str) -> None:
     if status != 0:
         lib = load()
         msg = lib.bcfft_status_string(status).decode()
-        hip = lib.bcfft_last_hip_error().decode()
-        raise RuntimeError(f"{what} failed: {msg}" + (f" ({hip})" if hip else ""))
+        hip = lib.bcfft_last_hip_error().decode() if status == 5 else ""
+        detail = lib.bcfft_last_error_detail().decode() if status == 2 else ""
+        raise RuntimeError(f"{what} failed: {msg}" + (f" ({hip})" if hip else "") + (f" [{detail}]" if detail else ""))
 
 
 def dtype_code(dt: torch.dtype) -> int:

@@ -76,7 +76,8 @@ def forward_glu(x2d: torch.Tensor, spec_gu: torch.Tensor, block_size: int, gate_
     the DFT kernel at b = 128 with K = 4096, else stationary), or "stationary" / "dft" / "dftx"."""
     algo = default_algo() if algo is None else algo
     if algo not in ("auto", "stationary", "dft", "dftx"):
-        algo = "auto"                               # mfma / valu have no fused gate/up form
+        raise ValueError(f"bcfft.forward_glu: engine {algo!r} has no fused gate/up form "
+                         "(auto, stationary, dft, dftx); run gate and up as two forwards instead")
     _lib.require_device(x2d, "bcfft.forward_glu")
     n, k = x2d.shape
     if block_size > 0 and gate_features % block_size == 0 and k % block_size == 0:
@@ -113,8 +114,8 @@ def default_algo() -> str:
 def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, block_size: int,
             out_features: int, algo: str | None = None) -> torch.Tensor:
     """y = BC(x2d) (+ bias) with one fused kernel. x2d: (N, K) device tensor.
-    algo: "auto" (dft where eligible, else stationary where eligible, else mfma for b <= 128,
-    else valu), "dft" (block DFTs and MAC on fp16 MFMA, weights in VGPRs, ~3.5e-4), "dftx"
+    algo: "auto" (at b = 128, K = 4096: dftx for fp32 outputs, dft for 16-bit ones; dft on its
+    other geometries; else stationary where eligible, else mfma for b <= 128, else valu), "dft" (block DFTs and MAC on fp16 MFMA, weights in VGPRs, ~3.5e-4), "dftx"
     (dft with the per-bin products split hi + lo: ~2.8e-4, linear to ~1e-6),
     "stationary" (weights in VGPRs, fp16 MFMA, ~3e-4), "mfma" (split-bf16, ~1e-5) or
     "valu" (exact fp32 MAC). See include/bcfft.h."""
@@ -138,7 +139,8 @@ def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, bl
     lib = _lib.load()
     code = _lib.ALGOS[(algo or default_algo()).lower()]
     # split-K workspace (short grids of the MFMA kernel); caller-owned, from torch's allocator
-    ws_bytes = lib.bcfft_forward_workspace_bytes(n, k, out_features, block_size, code)
+    ws_bytes = lib.bcfft_forward_workspace_bytes_io(n, k, out_features, block_size, code,
+                                                    _lib.dtype_code(x2d.dtype), _lib.dtype_code(out_dtype))
     ws = torch.empty(max(ws_bytes, 0), dtype=torch.uint8, device=x2d.device) if ws_bytes > 0 else None
     _lib.check(lib.bcfft_forward_ws(x2d.data_ptr(), _lib.dtype_code(x2d.dtype), n, k, out_features,
                                     block_size, spec.data_ptr(), bias_ptr, bias_code, y.data_ptr(),

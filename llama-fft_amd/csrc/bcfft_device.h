@@ -124,8 +124,12 @@ __device__ __forceinline__ float wave_max(float v) {
   return fmaxf(a, b);
 }
 
-// scale exponent for fp16 hi/lo: 2^nsc mx < 2^15, clamped so 2^nsc and 2^-nsc stay normal
+// scale exponent for fp16 hi/lo: 2^nsc mx < 2^15, clamped so 2^nsc and 2^-nsc stay normal. An
+// all-zero piece (mx == 0; frexp gives exponent 0) takes the largest exponent, i.e. "quieter than
+// anything": the kernels align a token's pieces to the smallest exponent among them, so a zero
+// piece must never become that reference (a quiet piece aligned to it would flush to zero).
 __device__ __forceinline__ int stat_scale_exp(float mx) {
+  if (mx == 0.f) return 126;
   const int nsc = 15 - __builtin_amdgcn_frexp_expf(mx);
   return nsc < -126 ? -126 : (nsc > 126 ? 126 : nsc);
 }

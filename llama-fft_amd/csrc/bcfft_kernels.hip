@@ -579,6 +579,29 @@ __global__ void circulant_matvec_kernel(const void* __restrict__ c, const void* 
 // ====================================================================== C ABI
 namespace {
 thread_local char g_last_hip_error[256] = {0};
+thread_local char g_last_detail[256] = {0};     // why the last call was refused (engine, geometry)
+
+const char* dt_name(int d) {
+  return d == BCFFT_F32 ? "fp32" : d == BCFFT_F16 ? "fp16" : d == BCFFT_BF16 ? "bf16" : d == BCFFT_NONE ? "none" : "?";
+}
+const char* algo_name(int a) {
+  switch (a) {
+    case BCFFT_ALGO_AUTO: return "auto";
+    case BCFFT_ALGO_MFMA: return "mfma";
+    case BCFFT_ALGO_VALU: return "valu";
+    case BCFFT_ALGO_STAT: return "stationary";
+    case BCFFT_ALGO_DFT: return "dft";
+    case BCFFT_ALGO_DFTX: return "dftx";
+    default: return "?";
+  }
+}
+// BCFFT_ERR_BLOCK with the refused engine and geometry in bcfft_last_error_detail()
+int refuse(const char* what, int algo, int n_in, int b, int xdt, int ydt) {
+  snprintf(g_last_detail, sizeof(g_last_detail),
+           "%s: engine '%s' does not serve block_size %d with %d input blocks (in_features %d), x %s -> y %s",
+           what, algo_name(algo), b, n_in, n_in * b, dt_name(xdt), dt_name(ydt));
+  return BCFFT_ERR_BLOCK;
+}
 
 int record_launch() {
   hipError_t e = hipGetLastError();
@@ -698,7 +721,7 @@ const char* bcfft_status_string(int status) {
   switch (status) {
     case BCFFT_OK: return "ok";
     case BCFFT_ERR_SHAPE: return "shape error: features must be positive multiples of block_size";
-    case BCFFT_ERR_BLOCK: return "unsupported block_size (supported: 32, 64, 128, 256)";
+    case BCFFT_ERR_BLOCK: return "block_size / engine not supported for this geometry (block sizes: 32, 64, 128, 256)";
     case BCFFT_ERR_DTYPE: return "unsupported dtype or y dtype != promote(x dtype, bias dtype)";
     case BCFFT_ERR_ALIGN: return "x, y, spectra and bias must be 16-byte aligned";
     case BCFFT_ERR_HIP: return "HIP launch failed";
@@ -708,6 +731,8 @@ const char* bcfft_status_string(int status) {
 }
 
 const char* bcfft_last_hip_error(void) { return g_last_hip_error; }
+
+const char* bcfft_last_error_detail(void) { return g_last_detail; }
 
 int64_t bcfft_spectra_bytes(int n_out_blocks, int n_in_blocks, int block_size) {
   if (n_out_blocks <= 0 || n_in_blocks <= 0 || !valid_block(block_size)) return -1;
@@ -733,11 +758,15 @@ int bcfft_spectra(const void* c, int c_dtype, int n_out_blocks, int n_in_blocks,
   return record_launch();
 }
 
-// the algorithm bcfft_forward_algo runs for this geometry (AUTO resolved)
-// (n_tokens < 0: unknown, as for the workspace query, whose DFT choices take no workspace)
-static int resolve_algo(int algo, int n_in, int block_size, int xdt = -1, bool yf32 = true, int64_t n_tokens = -1) {
+// the algorithm bcfft_forward_algo runs for this geometry (AUTO resolved). xdt = -2: the caller
+// did not say (bcfft_forward_workspace_bytes); the I/O-dependent choices are then not taken.
+// fp32 outputs take DFTX at b = 128 (its hi + lo products keep the layer linear in x to ~1e-6,
+// which fp32 training gradients through dx rely on); 16-bit outputs take the one-term DFT, whose
+// noise sits far below their own rounding.
+static int resolve_algo(int algo, int n_in, int block_size, int xdt = -2, bool yf32 = true, int64_t n_tokens = -1) {
   if (algo != BCFFT_ALGO_AUTO) return algo;
-  if (bcfft::dm_eligible(n_in, block_size) || bcfft::dm64_eligible(n_in, block_size, xdt, yf32)) return BCFFT_ALGO_DFT;
+  if (bcfft::dm_eligible(n_in, block_size)) return yf32 ? BCFFT_ALGO_DFTX : BCFFT_ALGO_DFT;
+  if (bcfft::dm64_eligible(n_in, block_size, xdt, yf32)) return BCFFT_ALGO_DFT;
   // K > 4096 at b = 128 (bf16): the streamed-weight DFT kernel, from one token up (it beats the
   // split-K MFMA kernel at every measured N: 20.9 vs 23.4 us at N = 1, profiles/r02_dmk_decode_sizes.log)
   if (bcfft::dmk_eligible(n_in, block_size, xdt, yf32) && n_tokens >= BCFFT_DMK_MIN_TOKENS) return BCFFT_ALGO_DFT;
@@ -745,13 +774,15 @@ static int resolve_algo(int algo, int n_in, int block_size, int xdt = -1, bool y
                                                 : (block_size <= 128 ? BCFFT_ALGO_MFMA : BCFFT_ALGO_VALU);
 }
 
-int64_t bcfft_forward_workspace_bytes(int64_t n_tokens, int in_features, int out_features, int block_size,
-                                      int algo) {
+static int64_t ws_bytes_for(int64_t n_tokens, int in_features, int out_features, int block_size, int algo,
+                               int xdt, bool yf32) {
   if (!valid_block(block_size) || n_tokens < 0 || in_features <= 0 || out_features <= 0 ||
       in_features % block_size || out_features % block_size)
     return -1;
   const int n_in = in_features / block_size;
-  const int a = resolve_algo(algo, n_in, block_size);
+  const int a = resolve_algo(algo, n_in, block_size, xdt, yf32, n_tokens);
+  // the DFT engines never take a workspace (the down projection's streamed-weight kernel included)
+  if (a == BCFFT_ALGO_DFT || a == BCFFT_ALGO_DFTX || a == BCFFT_ALGO_STAT) return 0;
   int kz = 1;
   if (a == BCFFT_ALGO_MFMA && block_size <= BCFFT_MFMA_MAXB) kz = mfma_ksplit(n_tokens, n_in, block_size);
   else if (a == BCFFT_ALGO_VALU || a == BCFFT_ALGO_MFMA) kz = valu_ksplit(n_tokens, n_in, block_size);
@@ -759,11 +790,23 @@ int64_t bcfft_forward_workspace_bytes(int64_t n_tokens, int in_features, int out
   return kz * n_tokens * (int64_t)out_features * (int64_t)sizeof(float);   // one fp32 slab per slice
 }
 
+int64_t bcfft_forward_workspace_bytes(int64_t n_tokens, int in_features, int out_features, int block_size,
+                                      int algo) {
+  return ws_bytes_for(n_tokens, in_features, out_features, block_size, algo, -2, true);
+}
+
+int64_t bcfft_forward_workspace_bytes_io(int64_t n_tokens, int in_features, int out_features, int block_size,
+                                         int algo, int x_dtype, int y_dtype) {
+  if (!valid_dt(x_dtype) || !valid_dt(y_dtype)) return -1;
+  return ws_bytes_for(n_tokens, in_features, out_features, block_size, algo, x_dtype, y_dtype == BCFFT_F32);
+}
+
 int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_features,
                      int out_features, int block_size, const void* spectra, const void* bias,
                      int bias_dtype, void* y, int y_dtype, int algo, void* workspace,
                      int64_t workspace_bytes, void* stream) {
-  if (!valid_block(block_size)) return BCFFT_ERR_BLOCK;
+  g_last_detail[0] = 0;
+  if (!valid_block(block_size)) return refuse("bcfft_forward", algo, 0, block_size, x_dtype, y_dtype);
   if (n_tokens < 0 || in_features <= 0 || out_features <= 0 || in_features % block_size ||
       out_features % block_size)
     return BCFFT_ERR_SHAPE;
@@ -781,14 +824,17 @@ int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_featur
     return BCFFT_ERR_ALIGN;
   const int n_in = in_features / block_size, n_out = out_features / block_size;
   const bool stat_ok = bcfft::stat_eligible(n_in, block_size);
-  if (algo == BCFFT_ALGO_STAT && !stat_ok) return BCFFT_ERR_BLOCK;
+  if (algo == BCFFT_ALGO_STAT && !stat_ok) return refuse("bcfft_forward", algo, n_in, block_size, x_dtype, y_dtype);
   const bool dm64 = bcfft::dm64_eligible(n_in, block_size, x_dtype, y_dtype == BCFFT_F32);
-  if (algo == BCFFT_ALGO_DFTX && !bcfft::dm_eligible(n_in, block_size)) return BCFFT_ERR_BLOCK;
+  if (algo == BCFFT_ALGO_DFTX && !bcfft::dm_eligible(n_in, block_size))
+    return refuse("bcfft_forward", algo, n_in, block_size, x_dtype, y_dtype);
   const bool dmk = bcfft::dmk_eligible(n_in, block_size, x_dtype, y_dtype == BCFFT_F32);
-  if (algo == BCFFT_ALGO_DFT && !bcfft::dm_eligible(n_in, block_size) && !dm64 && !dmk) return BCFFT_ERR_BLOCK;
+  if (algo == BCFFT_ALGO_DFT && !bcfft::dm_eligible(n_in, block_size) && !dm64 && !dmk)
+    return refuse("bcfft_forward", algo, n_in, block_size, x_dtype, y_dtype);
   algo = resolve_algo(algo, n_in, block_size, x_dtype, y_dtype == BCFFT_F32, n_tokens);
-  // the workspace is used only when it is as large as bcfft_forward_workspace_bytes asks
-  const int64_t need = bcfft_forward_workspace_bytes(n_tokens, in_features, out_features, block_size, algo);
+  // the workspace is used only when it is as large as bcfft_forward_workspace_bytes_io asks
+  const int64_t need = ws_bytes_for(n_tokens, in_features, out_features, block_size, algo, x_dtype,
+                                       y_dtype == BCFFT_F32);
   float* ws = (workspace && need > 0 && workspace_bytes >= need) ? (float*)workspace : nullptr;
   hipStream_t s = (hipStream_t)stream;
   if (algo == BCFFT_ALGO_DFT && dmk) {
@@ -827,20 +873,25 @@ int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_feat
 
 int bcfft_forward_glu_algo(const void* x, int x_dtype, int64_t n_tokens, int in_features, int gate_features,
                            int block_size, const void* spectra_gu, void* h, int algo, void* stream) {
+  g_last_detail[0] = 0;
   if (algo != BCFFT_ALGO_AUTO && algo != BCFFT_ALGO_STAT && algo != BCFFT_ALGO_DFT && algo != BCFFT_ALGO_DFTX)
     return BCFFT_ERR_ARG;
-  if (!valid_block(block_size)) return BCFFT_ERR_BLOCK;
+  if (!valid_block(block_size)) return refuse("bcfft_forward_glu", algo, 0, block_size, x_dtype, x_dtype);
   if (n_tokens < 0 || in_features <= 0 || gate_features <= 0 || in_features % block_size ||
       gate_features % block_size)
     return BCFFT_ERR_SHAPE;
   if (!valid_dt(x_dtype)) return BCFFT_ERR_DTYPE;
   const int n_in = in_features / block_size, n_gate = gate_features / block_size;
-  if (!bcfft::stat_eligible(n_in, block_size)) return BCFFT_ERR_BLOCK;
+  if (!bcfft::stat_eligible(n_in, block_size))
+    return refuse("bcfft_forward_glu", algo, n_in, block_size, x_dtype, x_dtype);
   const bool dm = bcfft::dm_eligible(n_in, block_size);
   const bool dm64 = bcfft::dm64_eligible(n_in, block_size, x_dtype, false);   // h has x's dtype
-  if (algo == BCFFT_ALGO_AUTO) algo = dm || dm64 ? BCFFT_ALGO_DFT : BCFFT_ALGO_STAT;
-  if (algo == BCFFT_ALGO_DFTX && !dm) return BCFFT_ERR_BLOCK;
-  if (algo == BCFFT_ALGO_DFT && !dm && !dm64) return BCFFT_ERR_BLOCK;
+  // AUTO: fp32 h takes the hi + lo products (DFTX), as bcfft_forward does for fp32 outputs
+  if (algo == BCFFT_ALGO_AUTO)
+    algo = dm ? (x_dtype == BCFFT_F32 ? BCFFT_ALGO_DFTX : BCFFT_ALGO_DFT) : dm64 ? BCFFT_ALGO_DFT : BCFFT_ALGO_STAT;
+  if (algo == BCFFT_ALGO_DFTX && !dm) return refuse("bcfft_forward_glu", algo, n_in, block_size, x_dtype, x_dtype);
+  if (algo == BCFFT_ALGO_DFT && !dm && !dm64)
+    return refuse("bcfft_forward_glu", algo, n_in, block_size, x_dtype, x_dtype);
   if (n_tokens == 0) return BCFFT_OK;
   if (!x || !h || !spectra_gu) return BCFFT_ERR_ARG;
   if (!aligned16(x) || !aligned16(h) || !aligned16(spectra_gu)) return BCFFT_ERR_ALIGN;

@@ -14,8 +14,9 @@ What differs, by design:
     parameter's version counter, so an in-place update of ``c`` can never be served stale
     (the reference's cached forward can: bench_all_in_one.py:204-216).
   * There is no CPU path: a non-ROCm tensor raises ``RuntimeError``.
-  * Backward: dL/dx runs the same fused kernel on the adjoint spectra; dL/dc uses torch.fft
-    on the device (scope row f3).
+  * Backward: dL/dx runs the same fused kernel on the adjoint spectra; dL/dc runs
+    ``bcfft_grad_c`` (bc_grad_c_kernel + bc_grad_c_finish: per-bin cross-correlation, fp64
+    split reduction; see DESIGN.md, scope row f3).
 """
 from __future__ import annotations
 
@@ -371,7 +372,9 @@ class BCFusedGateUp(nn.Module):
     def _fused_ok(self, x: torch.Tensor) -> bool:
         g, u = self._gate, self._up
         grad = torch.is_grad_enabled() and (g.c.requires_grad or u.c.requires_grad or x.requires_grad)
+        # BCFFT_ALGO=mfma / valu asks for an exact engine, which has no fused form: two launches
         return (g.bias is None and u.bias is None and not grad and x.is_cuda
+                and _ops.default_algo() not in ("mfma", "valu")
                 and _ops.glu_eligible(g.in_features, g.block_size))
 
     def _spectra(self) -> torch.Tensor:

@@ -18,7 +18,9 @@ def test_algorithmic_bytes_match_survey():
 
 
 def test_engine_resolution_mirrors_auto_rule():
-    assert bench.resolved_kernel("auto", 4096, 128)[1] == "bc_forward_dm_kernel"
+    assert bench.resolved_kernel("auto", 4096, 128)[:2] == ("dftx", "bc_forward_dm_kernel")   # fp32 out
+    assert bench.resolved_kernel("auto", 4096, 128, "fp16")[:2] == ("dft", "bc_forward_dm_kernel")
+    assert bench.resolved_kernel("dft", 4096, 128)[:2] == ("dft", "bc_forward_dm_kernel")
     assert bench.resolved_kernel("stationary", 4096, 128)[1] == "bc_forward_stat_kernel"
     assert bench.resolved_kernel("auto", 4096, 64)[1] == "bc_forward_stat_kernel"
     assert bench.resolved_kernel("auto", 2048, 64)[1] == "bc_forward_stat_kernel"

@@ -155,3 +155,38 @@ def test_forward_workspace_bytes_without_gpu(built_lib):
     assert fw(fake, F32, 8, 11008, 4096, 128, fake, None, NONE, fake, F32, AUTO, fake + 4, 1 << 20, None) == 4
     assert fw(None, F32, 0, 11008, 4096, 128, None, None, NONE, None, F32, AUTO, None, 0, None) == 0
     assert fw(fake, F32, 8, 4096, 4096, 128, fake, None, NONE, fake, F32, 9, None, 0, None) == 6
+
+
+def test_forward_workspace_bytes_io_follows_the_engine(built_lib):
+    """With the I/O dtypes known, AUTO resolves exactly as the forward will: the bf16 down
+    projection (streamed-weight DFT kernel) and b = 64 bf16 (DFT kernel) take no workspace, while
+    the same geometries with fp32 I/O still split K on the MFMA kernel."""
+    from bcfft import _lib
+    lib = _lib.load()
+    wio = lib.bcfft_forward_workspace_bytes_io
+    AUTO, MFMA = _lib.ALGOS["auto"], _lib.ALGOS["mfma"]
+    F32, BF16 = _lib.BCFFT_F32, _lib.BCFFT_BF16
+    assert wio(100, 11008, 4096, 128, AUTO, BF16, BF16) == 0
+    assert wio(100, 11008, 4096, 128, AUTO, F32, F32) == 6 * 100 * 4096 * 4
+    assert wio(100, 11008, 4096, 128, AUTO, BF16, F32) == 6 * 100 * 4096 * 4   # fp32 bias: not dmk
+    assert wio(100, 11008, 4096, 128, MFMA, BF16, BF16) == 6 * 100 * 4096 * 4  # forced MFMA splits
+    assert wio(100, 4096, 11008, 64, AUTO, BF16, BF16) == 0
+    assert wio(100, 4096, 4096, 128, AUTO, F32, F32) == 0
+    assert wio(100, 4096, 4096, 128, AUTO, 7, F32) == -1
+
+
+def test_refusal_names_engine_and_geometry(built_lib):
+    """BCFFT_ERR_BLOCK comes with the refused engine and geometry (bcfft_last_error_detail),
+    before anything is launched."""
+    from bcfft import _lib
+    lib = _lib.load()
+    fake, F32, NONE = 4096, _lib.BCFFT_F32, _lib.BCFFT_NONE
+    st = lib.bcfft_forward_ws(fake, F32, 8, 4096, 4096, 64, fake, None, NONE, fake, F32, _lib.ALGOS["dft"],
+                              None, 0, None)
+    assert st == 2
+    d = lib.bcfft_last_error_detail().decode()
+    assert "'dft'" in d and "block_size 64" in d and "64 input blocks" in d and "x fp32" in d, d
+    with pytest.raises(RuntimeError, match="engine 'dft' does not serve block_size 64"):
+        _lib.check(st, "bcfft_forward")
+    assert lib.bcfft_forward_ws(None, F32, 0, 4096, 4096, 128, None, None, NONE, None, F32, 0, None, 0, None) == 0
+    assert lib.bcfft_last_error_detail().decode() == ""
