@@ -478,12 +478,15 @@ inline int64_t group_grid(int64_t cus, int groups, int64_t n_mtiles) {
 // [packed fp32: nO*nI*H float2][twiddles: B float2][MFMA image (b <= 128)][stationary image]
 // MFMA image: dword ((c*H + f)*2 + prec)*nOp*8 + o*8 + j  = split-bf16 pair of bin f of
 // block (o, 8c + j): bin 0 (C0, C_H) as is, other bins conj(C); prec 0 = hi, 1 = lo.
-// Stationary image (stat_eligible geometries, bc_forward_stat_kernel): 16-B header
-// {s_C, 1/s_C, 0, 0} then, per output group of 32 blocks, per wave (8), per register piece,
-// per lane, the 16-B fp16 B fragment that lane keeps in VGPRs for the whole launch
-// (bcfft_stat.hip has the exact map).
+// Stationary image (stat_eligible geometries, bc_forward_stat_kernel): a 16-B header, then per
+// output group of 32 blocks, per wave (8), per register piece, per lane, the 16-B fp16 B fragment
+// that lane keeps in VGPRs for the whole launch (bcfft_stat.hip has the exact map), then the
+// inverse weight scales 1/s_o of the groups' 32 x groups output blocks (fp32, at osc_off_u32).
+// Output block o's fragments hold conj(S) s_o, s_o = 2^(15 - E_o) with max |S[o][.][.]| < 2^E_o:
+// every output block keeps fp16's full range, however quiet it is next to the others (one global
+// scale pushed the per-bin products of a 1e-4-quiet block into fp16 subnormals).
 struct SpecLayout {
-  int64_t packed_f2, tw_off_f2, img_off_u32, img_u32, stat_off_u32, stat_u32, total_bytes;
+  int64_t packed_f2, tw_off_f2, img_off_u32, img_u32, stat_off_u32, stat_u32, osc_off_u32, total_bytes;
   int n_chunk, n_out_pad, stat_groups, stat_pieces;
 };
 int device_cu_count();         // CUs of the current device (bcfft_stat.hip)
@@ -533,6 +536,8 @@ __host__ __device__ inline SpecLayout spec_layout(int n_out, int n_in, int b) {
     s.stat_pieces = 0;
     s.stat_u32 = 0;
   }
+  s.osc_off_u32 = s.stat_off_u32 + s.stat_u32;         // per-output-block inverse scales
+  s.stat_u32 += (int64_t)s.stat_groups * STAT_OUT_BLOCKS;
   s.total_bytes = (s.stat_off_u32 + s.stat_u32) * 4;
   return s;
 }

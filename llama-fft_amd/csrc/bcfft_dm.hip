@@ -44,7 +44,8 @@ constexpr int SLOT = 16384;                         // one token of a tile
 constexpr int REGION = TT * SLOT;                   // 64 KiB
 constexpr int F_OFF = 2 * REGION;                   // DFT table image, 64 rows x 256 B
 constexpr int SC_OFF = F_OFF + 16384;               // scale exponents [2 parity][4 token][2 half]
-constexpr int LDS_BYTES = SC_OFF + 64;
+constexpr int OS_OFF = SC_OFF + 64;                  // the group's 32 inverse weight scales
+constexpr int LDS_BYTES = OS_OFF + 128;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 
 // X unit (16 B = 4 input blocks x (re, im) fp16 of bin f, precision p, block quad q) of the
@@ -62,7 +63,7 @@ __device__ __forceinline__ int yunit(int w, int o, int par) { return w * 1024 + 
 template <int XT, bool YF32, bool EX, bool GLU>
 __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_out, const uint32_t* __restrict__ stat,
-    const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
+    const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
   using namespace dmk;
   constexpr int ES = XTraits<XT>::ES;
   constexpr bool Y32 = YF32 || XT == BCFFT_F32;
@@ -148,7 +149,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
       *reinterpret_cast<uint4*>(lds + F_OFF + 256 * t + 16 * (ch ^ fsw(t))) = tab[c];
     }
   }
-  const float inv_sc = __uint_as_float(stat[1]);
   f16x8 creg[BW][KS][NT];
   {
     const uint4* img = reinterpret_cast<const uint4*>(stat + 4) + ((int64_t)(grp_o * NW + wave) * NPIECE) * 64 + lane;
@@ -169,6 +169,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(creg[fb][ks][nt]));
   }
+  // the group's inverse weight scales 1 / s_o (per output block) -> LDS (after the weight loads: its wait must not hold them back)
+  if (tid < 32) reinterpret_cast<float*>(lds + OS_OFF)[tid] = osc[grp_o * 32 + tid];
   wait_vmcnt<0>();
   lds_barrier();
 #if defined(BCFFT_DM_PRIO) && BCFFT_DM_PRIO == 1          // experiment: I waves win arbitration
@@ -396,7 +398,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     char* slot = region + tslot * SLOT;
     const int* sc = wsc + par * 8 + tslot * 2;
     const int nmin = min(sc[0], sc[1]);
-    const float ysc = __builtin_ldexpf(inv_sc, 30 - nmin);
+    float ysc[NT];                                  // output block o = 16 nt + o16: 1 / s_o
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) ysc[nt] = __builtin_ldexpf(reinterpret_cast<const float*>(lds + OS_OFF)[16 * nt + o16], 30 - nmin);
     // all Y fragments of the token: B[k = 8 g + j][o] = unit(wave 4 ks + g, o, parity)
     constexpr int NYP = EX ? 2 : 1;                 // Y precision terms (hi; lo 8 KiB further)
     constexpr bool YSP_PREF_OFF = EX;               // the lo terms take the table prefetch's VGPRs
@@ -471,7 +475,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
           for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
             for (int r = 0; r < 4; ++r)             // gate / up rounded to x's dtype (:266)
-              gu[nt][hf][r] = round_to(hf ? fmaf(E[nt][r], ysc, -O[nt][r] * ysc) : fmaf(E[nt][r], ysc, O[nt][r] * ysc), XT);
+              gu[nt][hf][r] = round_to(hf ? fmaf(E[nt][r], ysc[nt], -O[nt][r] * ysc[nt]) : fmaf(E[nt][r], ysc[nt], O[nt][r] * ysc[nt]), XT);
         }
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
@@ -492,12 +496,12 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
         const int o = 16 * nt + o16;
         float os[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) os[r] = O[nt][r] * ysc;
+        for (int r = 0; r < 4; ++r) os[r] = O[nt][r] * ysc[nt];
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
           float v[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = hf ? fmaf(E[nt][r], ysc, -os[r]) : fmaf(E[nt][r], ysc, os[r]);
+          for (int r = 0; r < 4; ++r) v[r] = hf ? fmaf(E[nt][r], ysc[nt], -os[r]) : fmaf(E[nt][r], ysc[nt], os[r]);
           if (Y32 || bias_dt != BCFFT_NONE) {       // .to(x dtype) :266, + bias :270-271
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = round_to(v[r], XT);
@@ -640,8 +644,9 @@ void launch_dm(const void* x, int64_t n, int n_out, const void* spec, const void
   const int64_t n_mtiles = (n + 3) / 4;
   const int64_t total = bcfft::group_grid(bcfft::device_cu_count(), groups, n_mtiles);
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
+  const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
   hipLaunchKernelGGL((bcfft::bc_forward_dm_kernel<XT, YF32, EX, GLU>), dim3((unsigned)total), dim3(512), 0, s, x,
-                     n, n_out, stat, bias, bias_dt, y);
+                     n, n_out, stat, osc, bias, bias_dt, y);
 }
 }  // namespace
 

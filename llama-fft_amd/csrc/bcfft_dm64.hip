@@ -30,7 +30,8 @@ constexpr int SLOT = 8192 + 64;                     // one token
 constexpr int REGION = TT * SLOT;
 constexpr int F_OFF = 2 * REGION;                   // DFT table image, 32 rows x 128 B
 constexpr int SC_OFF = F_OFF + 4096;                // scale exponents [2 parity][8 token][4 quarter]
-constexpr int LDS_BYTES = SC_OFF + 256;
+constexpr int OS_OFF = SC_OFF + 256;                // the group's 32 inverse weight scales
+constexpr int LDS_BYTES = OS_OFF + 128;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 static_assert(F_OFF % 256 == 0, "table rows on the bank period");
 
@@ -47,7 +48,7 @@ __device__ __forceinline__ int yhalf64(int w, int o, int par) { return 2048 * pa
 template <bool GLU>
 __global__ __launch_bounds__(512, 2) void bc_forward_dm64_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_out, const uint32_t* __restrict__ stat,
-    const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
+    const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
   using namespace dm64;
   constexpr int XT = BCFFT_BF16;
   constexpr int ES = 2, ESY = 2;
@@ -94,7 +95,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64_kernel(
     const int t = tid >> 3, ch = tid & 7;
     *reinterpret_cast<uint4*>(lds + F_OFF + 128 * t + 16 * (ch ^ fsw64(t))) = tab[tid];
   }
-  const float inv_sc = __uint_as_float(stat[1]);
   f16x8 creg[BW][KS][NT];
   {
     const uint4* img = reinterpret_cast<const uint4*>(stat + 4) + ((int64_t)(grp_o * NW + wave) * NPIECE) * 64 + lane;
@@ -112,6 +112,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64_kernel(
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(creg[fb][ks][nt]));
   }
+  // the group's inverse weight scales 1 / s_o (per output block) -> LDS (after the weight loads: its wait must not hold them back)
+  if (tid < 32) reinterpret_cast<float*>(lds + OS_OFF)[tid] = osc[grp_o * 32 + tid];
   wait_vmcnt<0>();
   lds_barrier();
 
@@ -274,7 +276,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64_kernel(
     char* slot = region + wave * SLOT;
     const int* sc = wsc + par * 32 + wave * 4;
     const int nmin = min(min(sc[0], sc[1]), min(sc[2], sc[3]));
-    const float ysc = __builtin_ldexpf(inv_sc, 30 - nmin);
+    float ysc[NT];                                  // output block o = 16 nt + o16: 1 / s_o
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) ysc[nt] = __builtin_ldexpf(reinterpret_cast<const float*>(lds + OS_OFF)[16 * nt + o16], 30 - nmin);
     // Y fragments: B[k = 8 g + j][o] = bins 8g + par' + {0, 2} of wave 2g, {4, 6} of wave 2g + 1
     uint4 yf[2][NT];
 #pragma unroll
@@ -316,7 +320,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64_kernel(
           for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              gu[nt][hf][r] = round_to(hf ? fmaf(E[nt][r], ysc, -O[nt][r] * ysc) : fmaf(E[nt][r], ysc, O[nt][r] * ysc), XT);
+              gu[nt][hf][r] = round_to(hf ? fmaf(E[nt][r], ysc[nt], -O[nt][r] * ysc[nt]) : fmaf(E[nt][r], ysc[nt], O[nt][r] * ysc[nt]), XT);
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
           float v[4];
@@ -331,12 +335,12 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64_kernel(
           const int o = 16 * nt + o16;
           float os[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) os[r] = O[nt][r] * ysc;
+          for (int r = 0; r < 4; ++r) os[r] = O[nt][r] * ysc[nt];
 #pragma unroll
           for (int hf = 0; hf < 2; ++hf) {
             float v[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = hf ? fmaf(E[nt][r], ysc, -os[r]) : fmaf(E[nt][r], ysc, os[r]);
+            for (int r = 0; r < 4; ++r) v[r] = hf ? fmaf(E[nt][r], ysc[nt], -os[r]) : fmaf(E[nt][r], ysc[nt], os[r]);
             if (bias_dt != BCFFT_NONE) {            // .to(x dtype) :266, + bias :270-271
 #pragma unroll
               for (int r = 0; r < 4; ++r) v[r] = round_to(v[r], XT);
@@ -410,8 +414,9 @@ void launch_dm64(const void* x, int64_t n, int n_out, const void* spec, const vo
   const int64_t n_mtiles = (n + 7) / 8;
   const int64_t total = bcfft::group_grid(bcfft::device_cu_count(), groups, n_mtiles);
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
+  const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
   hipLaunchKernelGGL((bcfft::bc_forward_dm64_kernel<GLU>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_out, stat,
-                     bias, bias_dt, y);
+                     osc, bias, bias_dt, y);
 }
 }  // namespace
 

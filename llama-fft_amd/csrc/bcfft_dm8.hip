@@ -37,7 +37,8 @@ constexpr int SLOT = 8192 + 64;                     // one token
 constexpr int REGION = TT * SLOT;
 constexpr int F_OFF = 2 * REGION;                   // DFT table image, 64 rows x 256 B
 constexpr int SC_OFF = F_OFF + 16384;               // scale exponents [2 parity][8 token][2 half]
-constexpr int LDS_BYTES = SC_OFF + 128;
+constexpr int OS_OFF = SC_OFF + 128;                // the group's 32 inverse weight scales
+constexpr int LDS_BYTES = OS_OFF + 128;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 static_assert(F_OFF % 256 == 0, "table rows on the bank period");
 
@@ -52,7 +53,7 @@ __device__ __forceinline__ int yunit8(int w, int o, int par) { return 4096 * par
 template <bool GLU>
 __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_out, const uint32_t* __restrict__ stat,
-    const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
+    const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
   using namespace dm8;
   constexpr int XT = BCFFT_BF16;
   constexpr int ES = 2, ESY = 2;
@@ -110,7 +111,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
       *reinterpret_cast<uint4*>(lds + F_OFF + 256 * t + 16 * (ch ^ fsw(t))) = tab[c];
     }
   }
-  const float inv_sc = __uint_as_float(stat[1]);
   f16x8 creg[BW][KS][NT];
   {
     const uint4* img = reinterpret_cast<const uint4*>(stat + 4) + ((int64_t)(grp_o * NW + wave) * NPIECE) * 64 + lane;
@@ -129,6 +129,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(creg[fb][ks][nt]));
   }
+  // the group's inverse weight scales 1 / s_o (per output block) -> LDS (after the weight loads: its wait must not hold them back)
+  if (tid < 32) reinterpret_cast<float*>(lds + OS_OFF)[tid] = osc[grp_o * 32 + tid];
   wait_vmcnt<0>();
   lds_barrier();
 
@@ -300,7 +302,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
     char* slot = region + wave * SLOT;
     const int* sc = wsc + par * 16 + wave * 2;
     const int nmin = min(sc[0], sc[1]);
-    const float ysc = __builtin_ldexpf(inv_sc, 30 - nmin);
+    float ysc[NT];                                  // output block o = 16 nt + o16: 1 / s_o
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) ysc[nt] = __builtin_ldexpf(reinterpret_cast<const float*>(lds + OS_OFF)[16 * nt + o16], 30 - nmin);
     // all Y fragments of the token: B[k = 8 g + j][o] = yunit8(wave 4 ks + g, o, parity)
     uint4 yf[KS][2][NT];
     const char* yb = slot + 512 * g + 16 * o16;
@@ -359,7 +363,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
           for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
             for (int r = 0; r < 4; ++r)             // gate / up rounded to x's dtype (:266)
-              gu[nt][hf][r] = round_to(hf ? fmaf(E[nt][r], ysc, -O[nt][r] * ysc) : fmaf(E[nt][r], ysc, O[nt][r] * ysc), XT);
+              gu[nt][hf][r] = round_to(hf ? fmaf(E[nt][r], ysc[nt], -O[nt][r] * ysc[nt]) : fmaf(E[nt][r], ysc[nt], O[nt][r] * ysc[nt]), XT);
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
           float v[4];
@@ -374,12 +378,12 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
           const int o = 16 * nt + o16;
           float os[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) os[r] = O[nt][r] * ysc;
+          for (int r = 0; r < 4; ++r) os[r] = O[nt][r] * ysc[nt];
 #pragma unroll
           for (int hf = 0; hf < 2; ++hf) {
             float v[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = hf ? fmaf(E[nt][r], ysc, -os[r]) : fmaf(E[nt][r], ysc, os[r]);
+            for (int r = 0; r < 4; ++r) v[r] = hf ? fmaf(E[nt][r], ysc[nt], -os[r]) : fmaf(E[nt][r], ysc[nt], os[r]);
             if (bias_dt != BCFFT_NONE) {            // .to(x dtype) :266, + bias :270-271
 #pragma unroll
               for (int r = 0; r < 4; ++r) v[r] = round_to(v[r], XT);
@@ -465,8 +469,9 @@ void launch_dm8(const void* x, int64_t n, int n_out, const void* spec, const voi
   const int64_t n_mtiles = (n + 7) / 8;
   const int64_t total = bcfft::group_grid(bcfft::device_cu_count(), groups, n_mtiles);
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
+  const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
   hipLaunchKernelGGL((bcfft::bc_forward_dm8_kernel<GLU>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_out, stat,
-                     bias, bias_dt, y);
+                     osc, bias, bias_dt, y);
 }
 }  // namespace
 

@@ -65,7 +65,8 @@ struct Geo {
   static constexpr int F_OFF = 2 * REGION;          // DFT table image, 64 rows x 256 B
   static constexpr int SC_OFF = F_OFF + 16384;      // chunk scale exponents [TT]
   static constexpr int RR_OFF = SC_OFF + 64;        // per-token reference exponents [TT]
-  static constexpr int LDS_BYTES = RR_OFF + 64;
+  static constexpr int OS_OFF = RR_OFF + 64;       // the group's 32 inverse weight scales
+  static constexpr int LDS_BYTES = OS_OFF + 128;
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
   static_assert(F_OFF % 256 == 0, "table rows on the bank period");
 };
@@ -84,7 +85,7 @@ __device__ __forceinline__ uint32_t f16_pow2_neg(int d) {
 template <int TT>
 __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_in, int n_out, const uint32_t* __restrict__ stat,
-    const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
+    const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
   using namespace dmk;
   using G = Geo<TT>;
   constexpr int MT = G::MT, TPW = G::TPW, NDMA = G::NDMA, REGION = G::REGION, F_OFF = G::F_OFF;
@@ -413,7 +414,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
     const int l = opaque(lane);
     const int o16 = l & 15, g = l >> 4;
     char* slot = region + tl * YSLOT;
-    const float ysc = __builtin_ldexpf(__uint_as_float(stat[1]), 30 - rref);
+    float ysc[NT];                                  // output block o = 16 nt + o16: 1 / s_o
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) ysc[nt] = __builtin_ldexpf(reinterpret_cast<const float*>(lds + G::OS_OFF)[16 * nt + o16], 30 - rref);
     uint4 yf[2][2][NT];
     const char* yb = slot + 512 * g + 16 * o16;
 #pragma unroll
@@ -464,12 +467,12 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
         const int o = 16 * nt + o16;
         float os[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) os[r] = O[nt][r] * ysc;
+        for (int r = 0; r < 4; ++r) os[r] = O[nt][r] * ysc[nt];
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
           float v[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = hf ? fmaf(E[nt][r], ysc, -os[r]) : fmaf(E[nt][r], ysc, os[r]);
+          for (int r = 0; r < 4; ++r) v[r] = hf ? fmaf(E[nt][r], ysc[nt], -os[r]) : fmaf(E[nt][r], ysc[nt], os[r]);
           if (bias_dt != BCFFT_NONE) {              // .to(x dtype) :266, + bias :270-271
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = round_to(v[r], XT);
@@ -523,6 +526,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
       *reinterpret_cast<uint4*>(lds + F_OFF + 256 * t + 16 * (ch ^ fsw(t))) = tab[c];
     }
   }
+  // the group's inverse weight scales 1 / s_o (per output block) -> LDS
+  if (tid < 32) reinterpret_cast<float*>(lds + G::OS_OFF)[tid] = osc[grp_o * 32 + tid];
   wait_vmcnt<0>();
   lds_barrier();
   STAMP(0);
@@ -608,7 +613,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
 }
 
 // one thread per (group, chunk, wave, bin, N-tile, lane) 16-B fragment: 4 input blocks x
-// (re, im) fp16 of conj(S) * s_C (bin 0: (S_0, S_H) * s_C), zero outside the operator
+// (re, im) fp16 of conj(S) * s_o (bin 0: (S_0, S_H) * s_o), zero outside the operator
 __global__ void bc_dmk_image_kernel(int n_out, int n_in, float2* __restrict__ spec) {
   using namespace dmk;
   constexpr int H = B / 2;
@@ -617,7 +622,7 @@ __global__ void bc_dmk_image_kernel(int n_out, int n_in, float2* __restrict__ sp
   const int64_t total = (int64_t)sl.stat_groups * sl.stat_pieces * 64;
   uint32_t* hdr = reinterpret_cast<uint32_t*>(spec) + sl.stat_off_u32;
   uint4* img = reinterpret_cast<uint4*>(hdr + 4);
-  const float sc = __uint_as_float(hdr[0]);
+  const uint32_t* osc = reinterpret_cast<const uint32_t*>(spec) + sl.osc_off_u32;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int lane = (int)(idx & 63);
@@ -629,6 +634,7 @@ __global__ void bc_dmk_image_kernel(int n_out, int n_in, float2* __restrict__ sp
     const int gq = (int)(rest / (FRAGS * NW) / nch);
     const int f = w * BPW + fb;
     const int o = gq * NOG + nt * 16 + (lane & 15);
+    const float sc = __uint_as_float((254u << 23) - osc[o]);   // s_o = 1 / osc[o] (powers of two)
     const int i0 = c * 16 + 4 * (lane >> 4);
     uint32_t d[4];
 #pragma unroll
@@ -657,6 +663,7 @@ void launch_forward_dmk(const void* x, int64_t n, int n_in, int n_out, const voi
   const SpecLayout sl = spec_layout(n_out, n_in, 128);
   const int64_t cus = device_cu_count();
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
+  const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
   // A tile is a serial chain of chunk steps: the launch takes about (tiles per CU, rounded up)
   // x the tile time, ~21.7 us for 8 tokens and ~39.7 us for 16 at nI = 86 (16-token tiles
   // halve the weight stream per token). The smaller makespan wins; this model picks the faster
@@ -673,10 +680,10 @@ void launch_forward_dmk(const void* x, int64_t n, int n_in, int n_out, const voi
   const int64_t total = group_grid(cus, groups, n_mtiles);
   if (t16)
     hipLaunchKernelGGL(bc_forward_dmk_kernel<16>, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat,
-                       bias, bias_dt, y);
+                       osc, bias, bias_dt, y);
   else
     hipLaunchKernelGGL(bc_forward_dmk_kernel<8>, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat,
-                       bias, bias_dt, y);
+                       osc, bias, bias_dt, y);
 }
 
 void launch_dmk_image(int n_out, int n_in, void* spec, hipStream_t s) {

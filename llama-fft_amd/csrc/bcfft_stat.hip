@@ -64,7 +64,8 @@ struct GeoS {
   static constexpr int TWB_OFF = UCO_OFF + L * TS * 16;      // [B] float2      W_b^k
   static constexpr int SLOT_OFF = TWB_OFF + B * 8;           // [2][4] uint     token max |x|
   static constexpr int BIAS_OFF = SLOT_OFF + 32;             // [NOG * B] float  group's bias
-  static constexpr int LDS_BYTES = BIAS_OFF + NOG * B * 4;
+  static constexpr int OS_OFF = BIAS_OFF + NOG * B * 4;      // [NOG] float      1 / s_o
+  static constexpr int LDS_BYTES = OS_OFF + NOG * 4;
   static_assert(L == 2 || L == 4, "16 points per lane over 2 or 4 lanes");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
@@ -321,7 +322,7 @@ __device__ __forceinline__ int swz_x(int r) {
 template <int B, int KS, int XT, bool YF32, bool GLU>
 __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_out, const uint32_t* __restrict__ stat,
-    const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
+    const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
   using G = GeoS<B>;
   constexpr int H = G::H, L = G::L, BW = G::BW, NT = G::NT, TT = G::TT, NW = G::NW;
   constexpr int NI = 16 * KS, K = NI * B;
@@ -453,8 +454,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
   if (tid < 8) slots[tid] = 0u;
   lds_barrier();                                   // tables before the weight loads (pressure)
 
-  // ---- stationary B fragments: conj(C) * s_C as fp16, K/32 VGPRs per lane
-  const float inv_sc = __uint_as_float(stat[1]);
+  // ---- stationary B fragments: conj(C) * s_o as fp16, K/32 VGPRs per lane
   f16x8 creg[BW][KS][NT];
   {
     const uint4* img = reinterpret_cast<const uint4*>(stat + 4) + ((int64_t)(grp_o * NW + wave) * NPIECE) * 64 + lane;
@@ -476,6 +476,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
       bias_l[e] = col < (int64_t)n_out * B ? load_scalar(bias, col, bias_dt) : 0.f;
     }
   }
+  float* osc_l = reinterpret_cast<float*>(lds + G::OS_OFF);    // the group's 1 / s_o
+  if (tid < G::NOG) osc_l[tid] = osc[grp_o * G::NOG + tid];
 
 
   // A fragment unit (16 B: 4 blocks x (re, im) fp16 of bin f, precision prec, block quad lq)
@@ -860,8 +862,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
       lane_dft_dpp<L, true>(v, g);
     }
     MARK(inv_out);
-    // y[32 k1 + 2 k2 + {0,1}] = D (R0, R1) / s_C, D = stat_decode<L, true>(g)
-    const float sc = inv_sc;
+    // y[32 k1 + 2 k2 + {0,1}] = D (R0, R1) / s_o, D = stat_decode<L, true>(g)
+    const float sc = osc_l[inv_o];
     const bool rot = L == 4 && g == 3;              // stored = -i z
     const float sd = (g == 1 || g == 2) ? -sc : sc;
     const float c00 = rot ? 0.f : sd, c01 = rot ? -sc : 0.f;
@@ -954,35 +956,47 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
 }
 
 // ================================================================== weight preparation
-// s_C = 2^(15 - E), max |S| < 2^E over the packed spectra; header {s_C, 1/s_C}
+// Per output block o (one workgroup each, over the groups' 32 x groups blocks): the weight
+// scale s_o = 2^(15 - E_o) with max |S[o][.][.]| < 2^E_o over the block row's packed spectra
+// (an all-zero or padded row: s_o = 1). The image holds conj(S) s_o as fp16; the kernels scale
+// output block o by osc[o] = 1 / s_o. Header {1, 1, 0, 0} (kept for the layout).
 template <int B>
 __global__ void bc_stat_scale_kernel(int n_out, int n_in, float2* __restrict__ spec) {
   const SpecLayout sl = spec_layout(n_out, n_in, B);
-  const float* p = reinterpret_cast<const float*>(spec);
-  const int64_t n = sl.packed_f2 * 2;
+  const int o = blockIdx.x;
+  const float* p = reinterpret_cast<const float*>(spec) + (int64_t)o * n_in * B;   // row o: n_in x B/2 float2
+  const int64_t n = o < n_out ? (int64_t)n_in * B : 0;
   float mx = 0.f;
   for (int64_t e = threadIdx.x; e < n; e += blockDim.x) mx = fmaxf(mx, fabsf(p[e]));
-  __shared__ float red[1024];
+  __shared__ float red[256];
   red[threadIdx.x] = mx;
   __syncthreads();
-  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+  for (int st = blockDim.x / 2; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + st]);
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    const int e = __builtin_amdgcn_frexp_expf(red[0]);
-    int n2 = 15 - e;
-    n2 = n2 < -126 ? -126 : (n2 > 127 ? 127 : n2);
-    uint32_t* hdr = reinterpret_cast<uint32_t*>(spec) + sl.stat_off_u32;
-    hdr[0] = (uint32_t)((n2 + 127) << 23);
-    hdr[1] = (uint32_t)((127 - n2) << 23);
-    hdr[2] = 0u;
-    hdr[3] = 0u;
+    int n2 = red[0] > 0.f ? 15 - __builtin_amdgcn_frexp_expf(red[0]) : 0;
+    n2 = n2 < -126 ? -126 : (n2 > 126 ? 126 : n2);
+    reinterpret_cast<uint32_t*>(spec)[sl.osc_off_u32 + o] = (uint32_t)((127 - n2) << 23);   // 2^-n2
+    if (o == 0) {
+      uint32_t* hdr = reinterpret_cast<uint32_t*>(spec) + sl.stat_off_u32;
+      hdr[0] = 0x3f800000u;
+      hdr[1] = 0x3f800000u;
+      hdr[2] = 0u;
+      hdr[3] = 0u;
+    }
   }
+}
+void launch_stat_scale(int b, int n_out, int n_in, void* spec, hipStream_t s) {
+  const SpecLayout sl = spec_layout(n_out, n_in, b);
+  const unsigned blocks = (unsigned)(sl.stat_groups * STAT_OUT_BLOCKS);
+  if (b == 128) hipLaunchKernelGGL(bc_stat_scale_kernel<128>, dim3(blocks), dim3(256), 0, s, n_out, n_in, (float2*)spec);
+  else hipLaunchKernelGGL(bc_stat_scale_kernel<64>, dim3(blocks), dim3(256), 0, s, n_out, n_in, (float2*)spec);
 }
 
 // one thread per (group, wave, piece, lane) 16-B fragment: 4 input blocks x (re, im) fp16 of
-// conj(S) * s_C (bin 0: (S_0, S_H) * s_C), zero outside the operator
+// conj(S) * s_o (bin 0: (S_0, S_H) * s_o), zero outside the operator
 template <int B>
 __global__ void bc_stat_image_kernel(int n_out, int n_in, float2* __restrict__ spec) {
   constexpr int H = B / 2, BW = H / 8, NT = 2, NW = 8;
@@ -992,7 +1006,7 @@ __global__ void bc_stat_image_kernel(int n_out, int n_in, float2* __restrict__ s
   const int64_t total = (int64_t)sl.stat_groups * NW * npiece * 64;
   uint32_t* hdr = reinterpret_cast<uint32_t*>(spec) + sl.stat_off_u32;
   uint4* img = reinterpret_cast<uint4*>(hdr + 4);
-  const float sc = __uint_as_float(hdr[0]);
+  const uint32_t* osc = reinterpret_cast<const uint32_t*>(spec) + sl.osc_off_u32;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int lane = (int)(idx & 63);
@@ -1003,6 +1017,7 @@ __global__ void bc_stat_image_kernel(int n_out, int n_in, float2* __restrict__ s
     const int nt = p % NT, ks = (p / NT) % ks_n, fb = p / NT / ks_n;
     const int f = w * BW + fb;
     const int o = gq * STAT_OUT_BLOCKS + nt * 16 + (lane & 15);
+    const float sc = __uint_as_float((254u << 23) - osc[o]);   // s_o = 1 / osc[o] (powers of two)
     const int i0 = ks * 16 + 4 * (lane >> 4);
     uint32_t d[4];
 #pragma unroll
@@ -1059,8 +1074,9 @@ void launch_stat(const void* x, int64_t n, int n_out, const void* spec, const vo
   if (total > groups * n_mtiles) total = groups * n_mtiles;
   if (total < groups) total = groups;
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
+  const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
   hipLaunchKernelGGL((bcfft::bc_forward_stat_kernel<B, KS, XT, YF32, GLU>), dim3((unsigned)total), dim3(512), 0, s,
-                     x, n, n_out, stat, bias, bias_dt, y);
+                     x, n, n_out, stat, osc, bias, bias_dt, y);
 }
 
 template <int B, int KS>
@@ -1100,8 +1116,8 @@ bool launch_forward_stat(int b, int n_in, int xdt, bool yf32, const void* x, int
 }
 
 void launch_stat_image(int b, int n_out, int n_in, void* spec, hipStream_t s) {
-  if (dmk_geometry(n_in, b)) {                      // same header, streamed per-chunk fragments
-    hipLaunchKernelGGL(bc_stat_scale_kernel<128>, dim3(1), dim3(1024), 0, s, n_out, n_in, (float2*)spec);
+  if (dmk_geometry(n_in, b)) {                      // same scales, streamed per-chunk fragments
+    launch_stat_scale(128, n_out, n_in, spec, s);
     launch_dmk_image(n_out, n_in, spec, s);
     return;
   }
@@ -1109,13 +1125,11 @@ void launch_stat_image(int b, int n_out, int n_in, void* spec, hipStream_t s) {
   const SpecLayout sl = spec_layout(n_out, n_in, b);
   const int64_t total = (int64_t)sl.stat_groups * 8 * sl.stat_pieces * 64;
   const unsigned blocks = (unsigned)((total + 255) / 256 < 65535 ? (total + 255) / 256 : 65535);
-  if (b == 128) {
-    hipLaunchKernelGGL(bc_stat_scale_kernel<128>, dim3(1), dim3(1024), 0, s, n_out, n_in, (float2*)spec);
+  launch_stat_scale(b, n_out, n_in, spec, s);
+  if (b == 128)
     hipLaunchKernelGGL(bc_stat_image_kernel<128>, dim3(blocks), dim3(256), 0, s, n_out, n_in, (float2*)spec);
-  } else {
-    hipLaunchKernelGGL(bc_stat_scale_kernel<64>, dim3(1), dim3(1024), 0, s, n_out, n_in, (float2*)spec);
+  else
     hipLaunchKernelGGL(bc_stat_image_kernel<64>, dim3(blocks), dim3(256), 0, s, n_out, n_in, (float2*)spec);
-  }
 }
 }  // namespace bcfft
 

@@ -53,24 +53,27 @@ def _split16(v):
 
 
 def _scale_exp(mx):
-    """stat_scale_exp: 15 - frexp exponent, clamped to [-126, 126]."""
+    """stat_scale_exp: 15 - frexp exponent, clamped to [-126, 126]; an all-zero piece 126."""
+    if mx == 0:
+        return 126
     e = np.frexp(np.float32(mx))[1]
     return int(np.clip(15 - e, -126, 126))
 
 
 def stat_image(c):
-    """conj(C)/(2b) s_C as fp16 values (the STAT image's arithmetic), packed bins, and 1/s_C."""
+    """conj(C)/(2b) s_o as fp16 values (the STAT image's arithmetic: one power-of-two scale per
+    output block o, bc_stat_scale_kernel), packed bins, and 1/s_o per output block (shape (nO, 1))."""
     b = c.shape[-1]
     h = b // 2
     xf = np.fft.rfft(c.astype(np.float64), axis=-1) / (2.0 * b)
     p = xf[..., :h].astype(np.complex64).astype(np.complex128)
     p[..., 0] = np.float32(xf[..., 0].real) + 1j * np.float32(xf[..., h].real)
-    mx = max(np.abs(p.real).max(), np.abs(p.imag).max())
-    n2 = int(np.clip(15 - np.frexp(np.float32(mx))[1], -126, 127))
-    sc = 2.0 ** n2
+    mx = np.maximum(np.abs(p.real), np.abs(p.imag)).reshape(p.shape[0], -1).max(axis=1)
+    n2 = np.array([int(np.clip(15 - np.frexp(np.float32(m))[1], -126, 126)) if m > 0 else 0 for m in mx])
+    sc = (2.0 ** n2)[:, None, None]
     re = (p.real * sc).astype(np.float32).astype(np.float16).astype(np.float64)
     im = (p.imag * sc).astype(np.float32).astype(np.float16).astype(np.float64)
-    return re, im, 1.0 / sc                                  # im of bins > 0 are Im(C) (not conj)
+    return re, im, 1.0 / sc[:, :, 0]                         # im of bins > 0 are Im(C) (not conj)
 
 
 def _rne16(v):

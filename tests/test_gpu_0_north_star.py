@@ -93,17 +93,18 @@ def test_north_star_bf16_all_tokens_vs_oracle(dev):
 
 def _structured_layer(dev, m, k, b, seed):
     """A LLaMA-like dense weight with very different block norms, projected by from_linear (the
-    GPU loss-aware projection): N(0, 0.02) entries, output-block rows scaled over 1e-3..1 and
-    input-block columns over 1e-2..1, plus a smooth low-rank part whose blocks have decaying
-    circulant spectra."""
+    GPU loss-aware projection): N(0, 0.02) entries with input-block columns scaled over 1e-2..1,
+    plus a smooth rank-1 part (blocks with decaying circulant spectra, dominated by the DC bin);
+    output-block rows of the sum scaled over 1e-4..1."""
     from patch_llama_fft import BlockCirculantLinear
     g = torch.Generator().manual_seed(seed)
     w = torch.randn(m, k, generator=g) * 0.02
-    rs = torch.logspace(-3, 0, m // b)[torch.randperm(m // b, generator=g)]
+    rs = torch.logspace(-4, 0, m // b)[torch.randperm(m // b, generator=g)]
     cs = torch.logspace(-2, 0, k // b)[torch.randperm(k // b, generator=g)]
-    w *= rs.repeat_interleave(b)[:, None] * cs.repeat_interleave(b)[None, :]
+    w *= cs.repeat_interleave(b)[None, :]
     t = torch.arange(max(m, k), dtype=torch.float32)
     w += 0.05 * torch.outer(torch.cos(t[:m] * 0.01), torch.exp(-t[:k] / 700.0))
+    w *= rs.repeat_interleave(b)[:, None]
     lin = torch.nn.Linear(k, m, bias=False)
     with torch.no_grad():
         lin.weight.copy_(w)
@@ -118,12 +119,33 @@ def _structured_tokens(n, k, seed):
     return x
 
 
+def _magnitude_norms(x, c):
+    """Per token, the norm of the layer evaluated on magnitudes: sum_i |C_oi[f]| |X_i[f]| per
+    output block and bin, through irfft's Parseval weights. It is the scale of the standard
+    floating-point error bound of the per-bin sums (|fl(sum a b) - sum a b| <= g sum |a||b|):
+    a token whose output is a near-cancellation of large terms is measured against it."""
+    n, k = x.shape
+    no, ni, b = c.shape
+    xf = np.abs(np.fft.rfft(x.reshape(n, ni, b).astype(np.float64), axis=-1))
+    cf = np.abs(np.fft.rfft(c.astype(np.float64), axis=-1))
+    mag = np.einsum("oif,nif->nof", cf, xf)
+    w = np.full(b // 2 + 1, 2.0)
+    w[0] = w[-1] = 1.0
+    return np.sqrt(np.einsum("nof,f->n", mag ** 2, w) / b)
+
+
 @pytest.mark.parametrize("algo,xdt", [("auto", "float32"), ("dftx", "float32"), ("dft", "float32"),
-                                      ("stationary", "float32"), ("auto", "bfloat16")])
+                                      ("stationary", "float32"), ("mfma", "float32"), ("auto", "bfloat16")])
 def test_structured_weights_per_block_and_token(dev, monkeypatch, algo, xdt):
-    """from_linear weights (output blocks ~1e3 apart in norm) through the forward: the relative
-    error of EVERY output block and EVERY token stays within the north star's 1e-3 (16-bit I/O:
-    the bf16 rounding floor, 4e-3), so no quiet block hides behind loud ones in a Frobenius norm."""
+    """from_linear weights (output blocks ~1e4 apart in norm) through the forward, errors reported
+    per output block and per token:
+      * every output block within the north star's 1e-3 (16-bit I/O: the bf16 floor, 4e-3), so no
+        quiet block hides behind loud ones in a Frobenius norm;
+      * every token within the same bound measured against its magnitude evaluation
+        (_magnitude_norms). The raw per-token relative error is printed: for tokens whose output
+        nearly cancels (the rank-1 part's projection of x close to zero) it is the weight
+        spectra's fp16 rounding (~2^-12) times that cancellation, ~1e-2 on the DFT engines here
+        and ~1e-4 on the split-bf16 'mfma' engine."""
     monkeypatch.setenv("BCFFT_ALGO", algo)
     m, k, b, n = 4096, 4096, 128, 512
     mod = _structured_layer(dev, m, k, b, seed=3)
@@ -141,12 +163,19 @@ def test_structured_weights_per_block_and_token(dev, monkeypatch, algo, xdt):
     r = ref.astype(np.float64).reshape(n, m // b, b)
     per_block = np.sqrt((d ** 2).sum(axis=(0, 2)) / (r ** 2).sum(axis=(0, 2)))
     pt = _per_token(g, ref)
+    mag = _magnitude_norms(xr, c)
+    pt_cond = np.linalg.norm(d.reshape(n, m), axis=1) / mag
     norms = np.sqrt((r ** 2).sum(axis=(0, 2)))
+    amp = mag / np.maximum(np.linalg.norm(ref.astype(np.float64), axis=1), 1e-30)
     print(f"{algo}/{xdt}: block norms span {norms.max() / norms.min():.1e}; worst block "
-          f"{per_block.max():.3e} (block {per_block.argmax()}), worst token {pt.max():.3e}")
-    assert norms.max() / norms.min() > 100.0          # the test really has quiet and loud blocks
+          f"{per_block.max():.3e} (block {per_block.argmax()}); worst token {pt.max():.3e} raw "
+          f"(cancellation x{amp[pt.argmax()]:.0f}), {pt_cond.max():.3e} vs its magnitude evaluation; "
+          f"Frobenius {rel_err(g, ref):.3e}")
+    assert norms.max() / norms.min() > 1000.0         # the test really has quiet and loud blocks
+    assert rel_err(g, ref) < (TOL[algo] if xdt == "float32" else 4e-3)
     assert per_block.max() < tol, (int(per_block.argmax()), per_block.max())
-    assert pt.max() < tol, (int(pt.argmax()), pt.max())
+    assert pt_cond.max() < tol, (int(pt_cond.argmax()), pt_cond.max())
+    assert pt.max() < 50 * tol                        # gross-error guard on the raw figure
 
 
 DFT_GOLDEN = [nm for nm in names("fwd_") if nm.startswith(("fwd_4096sq_b128", "fwd_up_4096x11008_b128"))]
