@@ -51,7 +51,7 @@ def algo_bytes(n, k, m, b, io, bias):
     return n * k * SZ[io] + n * m * SZ[io] + n_out * n_in * (b // 2 + 1) * 8 + (m * SZ[io] if bias else 0)
 
 
-def resolved_kernel(algo, k, b, io="fp32"):
+def resolved_kernel(algo, k, b, io="fp32", m=4096):
     """(algorithm, kernel symbol, MAC arithmetic) that BCFFT_ALGO=algo runs for this geometry and
     I/O dtype (the output has the I/O dtype); mirrors bcfft_forward_algo's AUTO rule
     (resolve_algo in csrc/bcfft_kernels.hip): at b = 128, K = 4096 fp32 outputs take dftx."""
@@ -63,6 +63,10 @@ def resolved_kernel(algo, k, b, io="fp32"):
     if io == "bf16" and algo in ("dft", "auto") and b == 64 and n_in == 64:
         return ("dft", "bc_forward_dm64_kernel",
                 "MFMA fp16 throughout, b=64, 8 tokens per tile, one-term spectra (bf16 I/O)")
+    if io == "bf16" and algo in ("dft", "auto") and dft_ok and m > 32 * b:
+        return ("dft", "bc_forward_dmg_kernel",
+                "MFMA fp16 throughout, 8 tokens per tile, stage 1 once per tile, every output group's "
+                "weight fragments streamed from L2 (bf16 I/O)")
     if io == "bf16" and algo in ("dft", "auto") and dft_ok:
         return ("dft", "bc_forward_dm8_kernel",
                 "MFMA fp16 throughout, 8 tokens per tile, one-term spectra (bf16 I/O)")
@@ -299,7 +303,7 @@ def run_variants(dev, algo, steps):
         os.environ["BCFFT_ALGO"] = algo
         vbytes = algo_bytes(vn, vk, vm, vb, vio, False)
         variants.append({"workload": f"{vk}->{vm} b={vb} N={vn} {vio}-io algo={va}",
-                         "engine": resolved_kernel(va, vk, vb, vio)[1].replace("bc_forward_", "").replace("_kernel", ""),
+                         "engine": resolved_kernel(va, vk, vb, vio, vm)[1].replace("bc_forward_", "").replace("_kernel", ""),
                          "ms": round(vkern, 4),
                          "GTok_elem_s": round(vn * vm / (vkern * 1e-3) / 1e9, 3),
                          "GB_s": round(vbytes / (vkern * 1e-3) / 1e9, 1),
@@ -448,7 +452,7 @@ def main(argv=None):
 
     spectra_ms = time_spectra(layer) if layer is not None else None
     tag = f"{k}x{m}_b{b}_n{n_local}_{io}"
-    kname = resolved_kernel(algo, k, b, io)
+    kname = resolved_kernel(algo, k, b, io, m)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_budget > 0 and not stub:
         cpu = cpu_baseline(k, m, b, io, bool(args.bias), args.cpu_budget)

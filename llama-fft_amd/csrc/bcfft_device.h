@@ -558,6 +558,11 @@ bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, bool exact, const vo
 bool launch_forward_dm_glu(int b, int n_in, int xdt, bool exact, const void* x, int64_t n, int n_gate,
                            const void* spec, void* h, hipStream_t s);
 bool dm8_eligible(int n_in, int b, int xdt, bool yf32);
+// several output groups at bf16 I/O (bcfft_dmg.hip): one workgroup runs a token tile's stage 1
+// once and loops over the groups with their weight fragments streamed from L2
+bool dmg_eligible(int n_in, int b, int xdt, bool yf32, int n_out, bool glu);
+void launch_forward_dmg(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt, void* y,
+                        bool glu, hipStream_t s);
 bool dm64_eligible(int n_in, int b, int xdt, bool yf32);
 void launch_forward_dm64(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt,
                          void* y, bool glu, hipStream_t s);

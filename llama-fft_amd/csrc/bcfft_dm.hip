@@ -673,8 +673,14 @@ bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, bool exact, const vo
   (exact ? launch_dm<XT, YF, true>(x, n, n_out, spec, bias, bias_dt, y, s)          \
          : launch_dm<XT, YF, false>(x, n, n_out, spec, bias, bias_dt, y, s))
 #ifndef BCFFT_NO_DM8
-  if (!exact && dm8_eligible(n_in, b, xdt, yf32)) {  // bf16 I/O: 8 tokens per tile (bcfft_dm8.hip)
-    launch_forward_dm8(x, n, n_out, spec, bias, bias_dt, y, false, s);
+  if (!exact && dm8_eligible(n_in, b, xdt, yf32)) {  // bf16 I/O: 8 tokens per tile
+#ifndef BCFFT_NO_DMG
+    if (dmg_eligible(n_in, b, xdt, yf32, n_out, false)) {   // several groups: x transformed once (bcfft_dmg.hip)
+      launch_forward_dmg(x, n, n_out, spec, bias, bias_dt, y, false, s);
+      return true;
+    }
+#endif
+    launch_forward_dm8(x, n, n_out, spec, bias, bias_dt, y, false, s);   // bcfft_dm8.hip
     return true;
   }
 #endif
@@ -699,6 +705,10 @@ bool launch_forward_dm_glu(int b, int n_in, int xdt, bool exact, const void* x, 
   } else {
     if (exact) launch_dm<BCFFT_BF16, false, true, true>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
 #ifndef BCFFT_NO_DM8
+#ifndef BCFFT_NO_DMG
+    else if (dmg_eligible(n_in, b, xdt, false, n_gate, true))
+      launch_forward_dmg(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, true, s);   // x transformed once per tile
+#endif
     else launch_forward_dm8(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, true, s);   // 8 tokens per tile
 #else
     else launch_dm<BCFFT_BF16, false, false, true>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);

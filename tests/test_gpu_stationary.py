@@ -89,13 +89,17 @@ def test_stationary_vs_oracle(dev, k, m, b, n, xdt, mdt, bias):
 
 
 def test_auto_resolution_for_eligible_shapes(dev):
-    """AUTO picks the DFT-on-MFMA kernel at 4096^2 b=128, and at b=64 the stationary kernel for
-    fp32 I/O and the b=64 DFT kernel for bf16 I/O: same bits as the explicit algorithm."""
+    """AUTO picks the DFT-on-MFMA kernel at 4096^2 b=128 (hi + lo products, dftx, for fp32 outputs;
+    the one-term dft for 16-bit ones), and at b=64 the stationary kernel for fp32 I/O and the b=64
+    DFT kernel for bf16 I/O: same bits as the explicit algorithm."""
     rng = np.random.default_rng(1)
     c = (rng.standard_normal((32, 32, 128)) * 0.01).astype(np.float32)
     x = rng.standard_normal((12, 4096)).astype(np.float32)
     ya, _ = _run(dev, x, c, None, "float32", "float32", algo="auto")
-    yd, _ = _run(dev, x, c, None, "float32", "float32", algo="dft")
+    yd, _ = _run(dev, x, c, None, "float32", "float32", algo="dftx")
+    assert torch.equal(ya, yd)
+    ya, _ = _run(dev, x, c, None, "bfloat16", "bfloat16", algo="auto")
+    yd, _ = _run(dev, x, c, None, "bfloat16", "bfloat16", algo="dft")
     assert torch.equal(ya, yd)
     c64 = (rng.standard_normal((64, 64, 64)) * 0.01).astype(np.float32)
     ya, _ = _run(dev, x, c64, None, "float32", "float32", algo="auto")
