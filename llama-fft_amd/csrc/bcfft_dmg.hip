@@ -36,6 +36,13 @@ namespace bcfft {
 
 namespace dmg {
 using namespace dmh;
+// analysis builds only (results are WRONG when set): 1 no B loads, 2 no stage-1 arithmetic, 4 no
+// stage-2 MFMAs, 8 no stage 3, 16 no x DMA, 32 no y stores
+#ifdef BCFFT_DMG_ABL
+constexpr int ABL = BCFFT_DMG_ABL;
+#else
+constexpr int ABL = 0;
+#endif
 
 constexpr int B = 128, NI = 32, KS = 2, NOG = 32, TT = 8, NW = 8;
 constexpr int BW = 8, NT = 2;                       // bins per wave, 16-wide N-tiles per group
@@ -85,6 +92,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmg_kernel(
   // ---- x of token `wave` of M-tile m -> its slot by LDS-DMA (bcfft_dm8.hip's: the buffer range
   // zero-fills tokens past n_tokens; the slot's unit swizzle is applied to the source offsets)
   auto dma_token = [&](int64_t m, char* region) {
+    if constexpr ((ABL & 16) != 0) return;
     const int64_t tok = m * TT + wave;
     const bool ok = tok < n_tokens;
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
@@ -116,7 +124,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmg_kernel(
                                              NPIECE * 1024, 0x00020000);
   };
   auto load_b1 = [&](const __amdgpu_buffer_rsrc_t& brs, int vo, int p, int fb, Breg& br) {
-    br[fb] = __builtin_amdgcn_raw_buffer_load_b128(brs, vo, ((fb * KS + pass_ks(p)) * NT + pass_nt(p)) * 1024, 0);
+    if constexpr ((ABL & 1) != 0) br[fb] = u32x4{(uint32_t)vo, (uint32_t)p, (uint32_t)fb, 0u};
+    else br[fb] = __builtin_amdgcn_raw_buffer_load_b128(brs, vo, ((fb * KS + pass_ks(p)) * NT + pass_nt(p)) * 1024, 0);
   };
   auto load_pass = [&](int g, int p, Breg& br) {
     const __amdgpu_buffer_rsrc_t brs = b_rsrc(g);
@@ -147,6 +156,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmg_kernel(
   // ---- stage 1 (wave w, token slot w): x rows -> X units (one fp16 term), in place, per half
   // (bcfft_dm8.hip's stage 1)
   auto stage1 = [&](char* region, int par) {
+    if constexpr ((ABL & 2) != 0) {
+      if (lane < 2) wsc[par * 16 + wave * 2 + lane] = 0;
+      return;
+    }
     const int l = opaque(lane);
     const int b16 = l & 15, g = l >> 4;
     char* slot = region + wave * SLOT;
@@ -289,7 +302,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmg_kernel(
 #pragma unroll
       for (int fb = 0; fb < BW; ++fb) {
         const f16x8 bf = __builtin_bit_cast(f16x8, br[fb]);
-        if (ks == 0)
+        if constexpr ((ABL & 4) != 0)
+          acc[fb] = ks == 0 ? f32x4{bf[0], bf[1], areg[fb][0][0], 0.f} : acc[fb] + f32x4{bf[0], bf[1], areg[fb][1][0], 0.f};
+        else if (ks == 0)
           acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(areg[fb][0], bf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         else
           acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(areg[fb][1], bf, acc[fb], 0, 0, 0);
@@ -316,6 +331,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmg_kernel(
   // ---- stage 3 of group g (wave w, token slot w of this tile): Y -> y rows staged in the slot
   // (32 rows x 256 B; GLU: 16 h rows) and stored as 1 KiB buffer stores (bcfft_dm8.hip's).
   auto stage3 = [&](char* region, int par, int64_t m, int g, auto&& before_stores) {
+    if constexpr ((ABL & 8) != 0) {
+      before_stores();
+      return;
+    }
     const int l = opaque(lane);
     const int o16 = l & 15, gq = l >> 4;
     char* slot = region + wave * SLOT;
@@ -431,7 +450,11 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmg_kernel(
     for (int q = 0; q < NQ; ++q) {
       uint4 v = *reinterpret_cast<const uint4*>(slot + 1024 * q + rdb[q & 1]);
       if (q & 2) v = make_uint4(v.z, v.w, v.x, v.y);   // rows with bit 3: 8-B halves swapped
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, vofs + q * 1024, 0, 0);
+      if constexpr ((ABL & 32) != 0) {
+        if (v.x == 0x7fc00001u && tok < 0) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, vofs, 0, 0);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, vofs + q * 1024, 0, 0);
+      }
     }
   };
 

@@ -4,8 +4,9 @@
 Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts 64 B per 128-B memory-side
 read request on gfx950, i.e. exactly half the bytes of a wide coalesced streaming read, so it
 is doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores. Both are in KiB.
-usage: python tools/pmc_traffic.py ROUND TAG=gpurun_out/pmc_DIR [TAG=DIR ...]
-       TAG is bench.py's workload tag, e.g. 4096x4096_b128_n8192_fp32"""
+usage: python tools/pmc_traffic.py ROUND TAG=gpurun_out/pmc_DIR[@ALGO] [TAG=DIR[@ALGO] ...]
+       TAG is bench.py's workload tag, e.g. 4096x4096_b128_n8192_fp32; ALGO the engine measured
+       (bench.py matches it against the engine AUTO resolves to)"""
 import collections
 import csv
 import glob
@@ -15,7 +16,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = ("bc_forward_dm_kernel", "bc_forward_dm8_kernel", "bc_forward_dmk_kernel", "bc_forward_dm64_kernel",
-           "bc_forward_stat_kernel", "bc_forward_mfma_kernel", "bc_forward_valu_kernel")
+           "bc_forward_dmg_kernel", "bc_forward_stat_kernel", "bc_forward_mfma_kernel", "bc_forward_valu_kernel")
 
 
 def collect(d):
@@ -36,6 +37,7 @@ def main():
     res = {}
     for arg in sys.argv[2:]:
         tag, d = arg.split("=", 1)
+        d, _, algo = d.partition("@")
         per = collect(d)
         for k, cs in per.items():
             if "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
@@ -47,6 +49,8 @@ def main():
                         "raw_FETCH_SIZE_KiB": cs["FETCH_SIZE"]["mean"],
                         "raw_WRITE_SIZE_KiB": cs["WRITE_SIZE"]["mean"],
                         "launches": cs["FETCH_SIZE"]["n"], "source": d}
+            if algo:
+                res[tag]["algo"] = algo
     path = os.path.join(ROOT, "profiles", f"pmc_traffic_{rnd}.json")
     json.dump(res, open(path, "w"), indent=1)
     print(json.dumps(res, indent=1))

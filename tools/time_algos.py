@@ -66,6 +66,9 @@ if __name__ == "__main__":
     if "--xcd" in sys.argv:                         # shapes with several output groups (+ fused gate/up)
         shapes = [(4096, 11008, 128, "bf16", 8192), (4096, 11008, 64, "bf16", 8192), (4096, 4096, 64, "bf16", 8192)]
         t_glu()
+    if "--cfg2" in sys.argv:                        # config 2 and its fused gate/up (bcfft_dmg.hip)
+        shapes = [(4096, 11008, 128, "bf16", 8192)]
+        t_glu()
     if "--downmid" in sys.argv:                     # the 8/16-token tile switch point
         shapes = [(11008, 4096, 128, "bf16", n) for n in (3000, 4096, 5000, 6144)]
     if "--b64down" in sys.argv:
