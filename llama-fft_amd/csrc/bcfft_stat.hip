@@ -991,7 +991,8 @@ __global__ void bc_stat_scale_kernel(int n_out, int n_in, float2* __restrict__ s
 void launch_stat_scale(int b, int n_out, int n_in, void* spec, hipStream_t s) {
   const SpecLayout sl = spec_layout(n_out, n_in, b);
   const unsigned blocks = (unsigned)(sl.stat_groups * STAT_OUT_BLOCKS);
-  if (b == 128) hipLaunchKernelGGL(bc_stat_scale_kernel<128>, dim3(blocks), dim3(256), 0, s, n_out, n_in, (float2*)spec);
+  if (b == 256) hipLaunchKernelGGL(bc_stat_scale_kernel<256>, dim3(blocks), dim3(256), 0, s, n_out, n_in, (float2*)spec);
+  else if (b == 128) hipLaunchKernelGGL(bc_stat_scale_kernel<128>, dim3(blocks), dim3(256), 0, s, n_out, n_in, (float2*)spec);
   else hipLaunchKernelGGL(bc_stat_scale_kernel<64>, dim3(blocks), dim3(256), 0, s, n_out, n_in, (float2*)spec);
 }
 
@@ -1121,12 +1122,14 @@ void launch_stat_image(int b, int n_out, int n_in, void* spec, hipStream_t s) {
     launch_dmk_image(n_out, n_in, spec, s);
     return;
   }
-  if (!stat_eligible(n_in, b)) return;
+  if (!stat_eligible(n_in, b) && !dm256_geometry(n_in, b)) return;
   const SpecLayout sl = spec_layout(n_out, n_in, b);
   const int64_t total = (int64_t)sl.stat_groups * 8 * sl.stat_pieces * 64;
   const unsigned blocks = (unsigned)((total + 255) / 256 < 65535 ? (total + 255) / 256 : 65535);
   launch_stat_scale(b, n_out, n_in, spec, s);
-  if (b == 128)
+  if (b == 256)
+    hipLaunchKernelGGL(bc_stat_image_kernel<256>, dim3(blocks), dim3(256), 0, s, n_out, n_in, (float2*)spec);
+  else if (b == 128)
     hipLaunchKernelGGL(bc_stat_image_kernel<128>, dim3(blocks), dim3(256), 0, s, n_out, n_in, (float2*)spec);
   else
     hipLaunchKernelGGL(bc_stat_image_kernel<64>, dim3(blocks), dim3(256), 0, s, n_out, n_in, (float2*)spec);

@@ -1,0 +1,72 @@
+"""GPU parity of the b = 256 DFT-on-MFMA kernel (bcfft_dm256.hip: K = 4096, bf16 I/O; the
+reference's default block size, patch_llama_fft.py:13). The 256-point transforms are built from
+the 128-point table on three virtual rows (tests/dm256_model.py restates the algebra); the
+checks are the oracle (~1 bf16 ulp, per-token scales) and AUTO's resolution to it."""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import rel_err
+from test_gpu_stationary import _check, _run
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    import bcfft
+    bcfft.load()
+    return torch.device("cuda:0")
+
+
+CASES = [
+    # (M, N, bias): K = 4096, b = 256, bf16 I/O
+    (4096, 37, False),        # one group of 16 output blocks; ragged last tile of 8
+    (4096, 1, True),          # one token, bf16 bias
+    (11008, 19, False),       # 43 output blocks: 3 groups, the last partial (11)
+    (2048, 300, True),        # 8 output blocks: a partial group; several tiles per workgroup
+    (4096, 2049, False),      # several tiles per workgroup on every CU
+]
+
+
+@pytest.mark.parametrize("m,n,bias", CASES)
+def test_dm256_vs_oracle(dev, m, n, bias):
+    k, b = 4096, 256
+    rng = np.random.default_rng(m + 3 * n)
+    c = (rng.standard_normal((m // b, k // b, b)) * 0.01).astype(np.float32)
+    bv = (rng.standard_normal(m) * 0.1).astype(np.float32) if bias else None
+    x = rng.standard_normal((n, k)).astype(np.float32)
+    y, ref = _run(dev, x, c, bv, "bfloat16", "bfloat16", algo="dft")
+    _check(y, ref, "bfloat16")
+    ya, _ = _run(dev, x, c, bv, "bfloat16", "bfloat16", algo="auto")
+    assert torch.equal(y, ya)                       # AUTO resolves to it
+    x[0] *= 300.0                                   # per-token power-of-two scale
+    x[n - 1, 1000:1100] *= 1e-3
+    x[n // 2, 4000] = 50.0                          # one loud channel in the last block
+    y, ref = _run(dev, x, c, bv, "bfloat16", "bfloat16", algo="dft")
+    g = y.float().cpu().numpy()
+    for t in sorted({0, n // 2, n - 1}):
+        assert rel_err(g[t], ref[t]) < 4e-3, (t, rel_err(g[t], ref[t]))
+
+
+def test_dm256_full_size_sweep_shape(dev):
+    """The block-size sweep's q/k/v/o shape at b = 256 (4096 -> 4096, N = 8192): every token
+    within ~1 bf16 ulp of the oracle, run-to-run bit equality."""
+    from bcfft import ops
+    from oracle import bc_oracle as O
+    k, m, b, n = 4096, 4096, 256, 8192
+    rng = np.random.default_rng(7)
+    c = O.round_to((rng.standard_normal((m // b, k // b, b)) * 0.01).astype(np.float32), O.BF16)
+    x = O.round_to(rng.standard_normal((n, k)).astype(np.float32), O.BF16)
+    spec = ops.spectra(torch.from_numpy(c).to(dev).to(torch.bfloat16))
+    xt = torch.from_numpy(x).to(dev).to(torch.bfloat16)
+    y = ops.forward(xt, spec, None, b, m, algo="auto")
+    assert torch.equal(y, ops.forward(xt, spec, None, b, m, algo="auto"))
+    g = y.float().cpu().numpy()
+    ref = O.bc_forward(x, c, None, x_dtype=O.BF16)
+    ulp = 2.0 ** -7
+    rms = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
+    bad = np.abs(g - ref) > 2 * ulp * np.abs(ref) + 2 * ulp * rms
+    assert not bad.any(), f"{int(bad.sum())} elements beyond ~1 ulp"
+    assert rel_err(g, ref) < 4e-3
