@@ -67,6 +67,10 @@ def resolved_kernel(algo, k, b, io="fp32", m=4096):
         return ("dft", "bc_forward_dm256_kernel",
                 "MFMA fp16 throughout, b=256 as three 128-point virtual rows, 8 tokens per tile, "
                 "16 output blocks per workgroup (bf16 I/O)")
+    if io == "bf16" and algo in ("dft", "auto") and b == 256 and 1 <= n_in <= 127:
+        return ("dft", "bc_forward_dm256k_kernel",
+                "MFMA fp16 throughout, b=256 as three 128-point virtual rows, 16-block K-chunks with "
+                "weight fragments streamed from L2 (bf16 I/O)")
     if io == "bf16" and algo in ("dft", "auto") and dft_ok and m > 32 * b:
         return ("dft", "bc_forward_dmg_kernel",
                 "MFMA fp16 throughout, 8 tokens per tile, stage 1 once per tile, every output group's "

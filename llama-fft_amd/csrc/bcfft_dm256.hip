@@ -452,29 +452,545 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256_kernel(
 
   // Pipeline (bcfft_dm8.hip's), two workgroup barriers per M-tile; iteration it: region R =
   // it & 1 holds tile m, R' tile m - stride:
-  //   P1  wave w: its x DMA landed -> stage 1 of token w of tile m in R; stage 3 of token w of
-  //       tile m - stride from R' (stores); LDS-DMA of x(m + stride, token w) into that slot | Ba |
+  //   P1  wave w: stage 3 of token w of tile m - stride from R' (stores); LDS-DMA of
+  //       x(m + stride, token w) into that slot; its own x(m) landed (a whole iteration after
+  //       its issue) -> stage 1 of token w of tile m in R                                 | Ba |
   //   P2  stage 2 of tile m in R (Y units over each wave's own X units)                     | Bb |
+  // The x(m) waits count the younger VMEM operations: 8 stage-3 stores, then NDMA DMA pieces.
   int64_t m = wg_in_grp;
   for (int it = 0; m < n_mtiles || it > 0; ++it, m += gstride) {
     char* region = lds + (it & 1) * REGION;
     char* other = lds + ((it + 1) & 1) * REGION;
     const int par = it & 1;
     const bool have = m < n_mtiles;
-    if (have) {
-      wait_vmcnt<0>();                              // this wave's x (and its older y stores)
-      stage1(region, par);
-    }
     if (it > 0) stage3(other, par ^ 1, m - gstride);
-    if (m + gstride < n_mtiles) {
+    const bool pf = m + gstride < n_mtiles;
+    if (pf) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
       dma_token(m + gstride, other);
     }
     if (!have) break;
+    if (pf) {
+      if (it > 0) wait_vmcnt<8 + NDMA>();
+      else wait_vmcnt<NDMA>();
+    } else {
+      if (it > 0) wait_vmcnt<8>();
+      else wait_vmcnt<0>();
+    }
+    stage1(region, par);
     lds_barrier();                                  // Ba: X units and scales complete
     stage2(region, par);
     lds_barrier();                                  // Bb: Y units complete
   }
+}
+
+// ============================================================== K > 4096: streamed weights
+// bc_forward_dm256k_kernel: b = 256 with more than 16 input blocks (the LLaMA down projection
+// 11008 -> 4096: 43 blocks). A workgroup's 16 output blocks x n_in input blocks of fp16 spectra
+// (88 KiB per 11 blocks) do not fit its VGPRs, so the K axis is cut into 16-block chunks
+// (bcfft_dmk.hip's scheme at b = 256): per chunk, stage 1 of the 8 tokens' chunk rows (x DMA one
+// chunk ahead), then stage 2 against the chunk's B fragments streamed from L2 (16 per wave, the
+// next chunk's loaded bin by bin into the same registers as each bin is done), accumulating in
+// 64 fp32 VGPRs over all chunks. At the tile end the Y units go into the last chunk's region and
+// stage 3 of token w runs at the start of the next tile, beside its first stage 1.
+// Numerics: per-(token, chunk) power-of-two scales with HEAD bits of headroom (stage 2 aligns
+// each chunk to the token's reference exponent with an exact fp16 power-of-two factor and scales
+// the accumulator rows down once if a chunk is more than 2^HEAD louder: tests/dm_model.py's
+// head = 4 scheme); otherwise bc_forward_dm256_kernel's.
+namespace d256 {
+constexpr int HEAD = 4;
+constexpr int SC2_OFF = CS_OFF + 1024;              // chunk scale exponents [8 tokens]
+constexpr int RR_OFF = SC2_OFF + 64;                // per-token reference exponents [8]
+constexpr int OS2_OFF = RR_OFF + 64;                // the workgroup's 16 inverse weight scales
+constexpr int LDS2_BYTES = OS2_OFF + 64;
+static_assert(LDS2_BYTES <= 160 * 1024, "LDS budget");
+constexpr int NDMA_C = NI * B * 2 / 1024;           // 1-KiB x DMA pieces per token and chunk
+// fp16 factor 2^-d (d >= -15) as a (lo, hi) pair: subnormal below 2^-14, zero below 2^-24
+__device__ __forceinline__ uint32_t f16_pow2_neg(int d) {
+  return d <= 14 ? (uint32_t)(15 - d) << 10 : (d <= 24 ? 1u << (24 - d) : 0u);
+}
+}  // namespace d256
+
+__global__ __launch_bounds__(512, 2) void bc_forward_dm256k_kernel(
+    const void* __restrict__ xv, int64_t n_tokens, int n_in, int n_out, const uint32_t* __restrict__ stat,
+    const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
+  using namespace d256;
+  constexpr int XT = BCFFT_BF16;
+  constexpr int ES = 2, ESY = 2;
+
+  __shared__ __attribute__((aligned(16))) char lds[LDS2_BYTES];
+  int* wsc = reinterpret_cast<int*>(lds + SC2_OFF);
+  int* wrr = reinterpret_cast<int*>(lds + RR_OFF);
+  const float2* cs_l = reinterpret_cast<const float2*>(lds + CS_OFF);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n_groups = (n_out + NOB - 1) / NOB;
+  const GroupMap gm = group_map(n_groups);
+  const int grp_o = gm.grp, wg_in_grp = gm.lane;
+  const int64_t KX = (int64_t)n_in * B;
+  const int64_t M = (int64_t)n_out * B;
+  const int nch = (n_in + NI - 1) / NI;
+  const int64_t n_mtiles = (n_tokens + TT - 1) / TT;
+  const int gstride = gm.stride;
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+
+  // ---- chunk c of token `wave` of M-tile m -> its slot by LDS-DMA (rows of 512 B, unit swizzle
+  // u ^ (r & 15)); the buffer range ends at the token's row end, so a partial last chunk and
+  // tokens / tiles past the end land as zeros
+  auto dma_chunk = [&](int64_t m, int c, char* region) {
+    const int64_t tok = m * TT + wave;
+    const bool ok = m < n_mtiles && tok < n_tokens;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>((const char*)xv) + (ok ? tok * KX * ES + (int64_t)c * (NI * B * ES) : 0), 0,
+        ok ? (int)(KX * ES - (int64_t)c * (NI * B * ES)) : 0, 0x00020000);
+    const int dl = opaque(lane);
+    const uint32_t dst0 = lds_base + (uint32_t)(region - lds) + wave * SLOT;
+    int vb[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int h = dl >> 5;
+      vb[q] = h * 512 + 16 * ((dl & 31) ^ ((2 * q + h) & 15));
+    }
+#pragma unroll
+    for (int q = 0; q < NDMA_C; ++q) {
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(vb[q & 7]), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
+    }
+  };
+
+  // ---- B fragments: STAT image group grp_o >> 1, wave, piece (fb KS + c) 2 + (grp_o & 1). Asm
+  // loads (bcfft_dmk.hip's scheme): the compiler does not count them, so its waits never drain
+  // the x DMA issued after them; wait_b is the one wait, with the exact number of younger VMEM
+  // operations, and it redefines the registers it waited for.
+  const int KS = nch;
+  const int npiece = BPW * KS * 2;
+  const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint32_t*>(stat + 4) + ((int64_t)((grp_o >> 1) * NW + wave) * npiece) * 256, 0, npiece * 1024,
+      0x00020000);
+  auto load_b1 = [&](int c, int fb, u32x4 (&breg)[BPW]) {
+    const int vo = opaque(lane) * 16 + (c * 2 + (grp_o & 1)) * 1024;
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen"
+                 : "=v"(breg[fb]) : "v"(vo), "s"(brs), "s"(fb * KS * 2048));
+  };
+  auto wait_b = [&](auto n_tag, u32x4 (&breg)[BPW]) {
+    constexpr int N = decltype(n_tag)::value;
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    asm volatile("s_waitcnt vmcnt(%16)"
+                 : "+v"(breg[0]), "+v"(breg[1]), "+v"(breg[2]), "+v"(breg[3]), "+v"(breg[4]), "+v"(breg[5]),
+                   "+v"(breg[6]), "+v"(breg[7]), "+v"(breg[8]), "+v"(breg[9]), "+v"(breg[10]), "+v"(breg[11]),
+                   "+v"(breg[12]), "+v"(breg[13]), "+v"(breg[14]), "+v"(breg[15])
+                 : "n"(N) : "memory");
+  };
+  static_assert(BPW == 16, "wait_b names sixteen fragments");
+
+  // ---- prologue: the first tile's chunk 0, the DFT and psi tables, the inverse weight scales
+  dma_chunk(wg_in_grp, 0, lds);
+  {
+    const uint4* tab = reinterpret_cast<const uint4*>(kDmF);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int c = tid + 512 * r;
+      const int t = c >> 4, ch = c & 15;
+      *reinterpret_cast<uint4*>(lds + F_OFF + 256 * t + 16 * (ch ^ fsw(t))) = tab[c];
+    }
+    if (tid < 128) {
+      double sn, cn;
+      sincospi((double)tid / 128.0, &sn, &cn);
+      reinterpret_cast<float2*>(lds + CS_OFF)[tid] = make_float2((float)cn, (float)sn);
+    }
+  }
+  if (tid < NOB) reinterpret_cast<float*>(lds + OS2_OFF)[tid] = osc[grp_o * NOB + tid];
+  wait_vmcnt<0>();
+  lds_barrier();
+
+  // ---- stage 1 (wave w, token slot w): bc_forward_dm256_kernel's on one 16-block chunk, with
+  // the per-(token, chunk) scale lowered by HEAD bits, and the odd-bin pass split by parity
+  auto stage1 = [&](char* region) {
+    const int l = opaque(lane);
+    const int b16 = l & 15, g = l >> 4;
+    char* slot = region + wave * SLOT;
+    const int q4 = (l & 15) >> 2, p4 = l & 3;
+    const int cx = (p4 >> 1) ^ fsw(8 * g + q4);
+    const int trb = F_OFF + 256 * (8 * g + q4) + 8 * (p4 & 1);
+    const char* rowp = slot + b16 * (B * ES);
+    uint32_t xr[4][2][4];
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const uint4 w = *reinterpret_cast<const uint4*>(rowp + 16 * ((8 * qt + 4 * ks + g) ^ b16));
+        xr[qt][ks][0] = w.x; xr[qt][ks][1] = w.y; xr[qt][ks][2] = w.z; xr[qt][ks][3] = w.w;
+      }
+    float m0f = 0.f, m1f = 0.f;
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const float2 f0 = unpack16<XT>(xr[qt][ks][e]), f1 = unpack16<XT>(xr[qt][ks][e + 1]);
+          m0f = amax3(m0f, f0.x, f0.y);
+          m1f = amax3(m1f, f1.x, f1.y);
+        }
+    const float mxf = __builtin_fmaxf(m0f, m1f);
+    const int sx = stat_scale_exp(4.f * __uint_as_float(wave_umax(__float_as_uint(mxf)))) - HEAD;
+    if (l == 0) wsc[wave] = sx - 7;                 // X = D 2^-(sx - 7): the table's 2^-7
+    const float S = __int_as_float((sx + 127) << 23);
+    uint32_t fa[2][2][4], fp[2][2][4], fq[2][2][4];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const float4* csp = reinterpret_cast<const float4*>(cs_l + 32 * ks + 8 * g);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float4 cs2 = csp[e];
+        const float2 x0 = unpack16<XT>(xr[0][ks][e]), x1 = unpack16<XT>(xr[1][ks][e]);
+        const float2 x2 = unpack16<XT>(xr[2][ks][e]), x3 = unpack16<XT>(xr[3][ks][e]);
+        float ap[2], app[2], pp[2], ppp[2], qp[2], qpp[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float xt = h ? x0.y : x0.x, xt64 = h ? x1.y : x1.x, xt128 = h ? x2.y : x2.x, xt192 = h ? x3.y : x3.x;
+          const float c = h ? cs2.z : cs2.x, s = h ? cs2.w : cs2.y;
+          const float u = (xt + xt128) * S, v = (xt64 + xt192) * S;
+          const float d0 = (xt - xt128) * S, d1 = (xt64 - xt192) * S;
+          ap[h] = u + v;
+          app[h] = u - v;
+          pp[h] = fmaf(d0, c, -d1 * s);
+          ppp[h] = fmaf(d0, c, d1 * s);
+          qp[h] = -fmaf(d0, s, d1 * c);
+          qpp[h] = fmaf(d1, c, -d0 * s);
+        }
+        fa[ks][0][e] = pk_rne(ap[0], ap[1]);
+        fa[ks][1][e] = pk_rne(app[0], app[1]);
+        fp[ks][0][e] = pk_rne(pp[0], pp[1]);
+        fp[ks][1][e] = pk_rne(ppp[0], ppp[1]);
+        fq[ks][0][e] = pk_rne(qp[0], qp[1]);
+        fq[ks][1][e] = pk_rne(qpp[0], qpp[1]);
+      }
+    }
+    {
+      f32x4 acc8[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc8[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) {
+            const int cb = 16 * ((8 * pr + 2 * mt) ^ cx);
+            const char* p0 = lds + trb + 256 * 32 * ks + cb;
+            const s16x4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p0));
+            const s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p0 + 256 * 4));
+            const f16x8 af = __builtin_bit_cast(f16x8, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+            acc8[4 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                af, frag(fa[ks][pr][0], fa[ks][pr][1], fa[ks][pr][2], fa[ks][pr][3]), acc8[4 * pr + mt], 0, 0, 0);
+          }
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const int f = 16 * mt + 4 * g + pr;
+          *reinterpret_cast<uint32_t*>(slot + xunit(2 * f, 0) + 4 * b16) = pk_rne(acc8[4 * pr + mt][0], acc8[4 * pr + mt][1]);
+          *reinterpret_cast<uint32_t*>(slot + xunit(2 * f + 4, 0) + 4 * b16) = pk_rne(acc8[4 * pr + mt][2], acc8[4 * pr + mt][3]);
+        }
+    }
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      f32x4 accp[4], accq[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        accp[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        accq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const int cb = 16 * ((8 * pr + 2 * mt) ^ cx);
+          const char* p0 = lds + trb + 256 * 32 * ks + cb;
+          const s16x4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p0));
+          const s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p0 + 256 * 4));
+          const f16x8 af = __builtin_bit_cast(f16x8, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+          accp[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+              af, frag(fp[ks][pr][0], fp[ks][pr][1], fp[ks][pr][2], fp[ks][pr][3]), accp[mt], 0, 0, 0);
+          accq[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+              af, frag(fq[ks][pr][0], fq[ks][pr][1], fq[ks][pr][2], fq[ks][pr][3]), accq[mt], 0, 0, 0);
+        }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const f32x4 P = accp[mt], Q = accq[mt];
+        const int f = 16 * mt + 4 * g + pr;
+        float re0 = P[0] - Q[1], im0 = P[1] + Q[0];
+        if (mt == 0 && pr == 0 && g == 0) {         // packed bin 0 = (P_0, P_64): X_1 = P_0 + i Q_0
+          re0 = P[0];
+          im0 = Q[0];
+        }
+        *reinterpret_cast<uint32_t*>(slot + xunit(2 * f + 1, 0) + 4 * b16) = pk_rne(re0, im0);
+        *reinterpret_cast<uint32_t*>(slot + xunit(2 * f + 5, 0) + 4 * b16) = pk_rne(P[2] - Q[3], P[3] + Q[2]);
+      }
+    }
+  };
+
+  // accumulators [bin of the wave]: rows 4 yt + r = token 2 yt + (r >> 1), re / im r & 1; the
+  // reference exponents of the lane's A-row token and accumulator-row tokens
+  f32x4 acc[BPW];
+#pragma unroll
+  for (int fb = 0; fb < BPW; ++fb) acc[fb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int ra = 0;
+  int rc[2] = {0, 0};
+
+  // ---- stage 2 (all waves): chunk c's per-bin complex MAC on bins 16 wave + fb, accumulated
+  // (the accumulators are zero at a tile's first chunk); the fragment of each bin for the next
+  // (tile, chunk) step is loaded into its registers right after its MFMA (nb < 0: none). One call
+  // site: the fragments stay in the same registers from their load to their use.
+  auto stage2 = [&](char* region, u32x4 (&breg)[BPW], int nb, bool first, bool tile0) {
+    const int ml = opaque(lane);
+    const int arow = ml & 15, kb = ml >> 4;
+    const int a_t = arow >> 1, a_reim = arow & 1;
+    const uint32_t a_sel = a_reim ? 0x01000302u : 0x03020100u;
+    const int yt = ml >> 4;
+    const int nka = wsc[a_t];
+    if (first) {
+      ra = nka;
+      rc[0] = wsc[2 * yt];
+      rc[1] = wsc[2 * yt + 1];
+    } else {
+      ra = min(ra, nka + HEAD);
+      float fct[2];
+      bool need = false;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int nn = wsc[2 * yt + s] + HEAD;
+        const int d = rc[s] - nn;
+        fct[s] = d > 0 ? __builtin_ldexpf(1.f, -d) : 1.f;
+        need |= d > 0;
+        rc[s] = min(rc[s], nn);
+      }
+      if (__builtin_amdgcn_ballot_w64(need)) {
+#pragma unroll
+        for (int fb = 0; fb < BPW; ++fb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[fb][r] *= fct[r >> 1];
+      }
+    }
+    const int d = nka - ra;                         // >= -HEAD: factor 2^-d <= 2^HEAD
+    const uint32_t hh = f16_pow2_neg(d);
+    const uint32_t h0 = f16_pow2_neg(d + 1);        // bin 0: the extra 1/2
+    const uint32_t amul = a_reim ? (hh | ((hh | 0x8000u) << 16)) : (hh | (hh << 16));
+    const uint32_t amul0 = a_reim ? (h0 << 16) : h0;
+    const char* ab = region + a_t * SLOT + 16 * kb;
+    // B of this step: the younger VMEM is this step's x DMA and, at a tile's first chunk, the
+    // previous tile's stage-3 stores before it
+    if (tile0) wait_b(std::integral_constant<int, 8 + NDMA_C>{}, breg);
+    else wait_b(std::integral_constant<int, NDMA_C>{}, breg);
+    const int nc = nb < 0 ? 0 : nb;
+#pragma unroll
+    for (int fb = 0; fb < BPW; ++fb) {
+      const int k = wave * BPW + fb;
+      uint4 raw = *reinterpret_cast<const uint4*>(ab + xunit(k, 0));
+      if (k == 0) {
+        raw.x = pkmul(raw.x, amul0); raw.y = pkmul(raw.y, amul0);
+        raw.z = pkmul(raw.z, amul0); raw.w = pkmul(raw.w, amul0);
+      } else {
+        raw.x = pkmul(__builtin_amdgcn_perm(raw.x, raw.x, a_sel), amul);
+        raw.y = pkmul(__builtin_amdgcn_perm(raw.y, raw.y, a_sel), amul);
+        raw.z = pkmul(__builtin_amdgcn_perm(raw.z, raw.z, a_sel), amul);
+        raw.w = pkmul(__builtin_amdgcn_perm(raw.w, raw.w, a_sel), amul);
+      }
+      acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, raw),
+                                                       __builtin_bit_cast(f16x8, breg[fb]), acc[fb], 0, 0, 0);
+      if (nb >= 0) load_b1(nc, fb, breg);
+    }
+  };
+
+  // ---- Y of the tile (fp16 units, bc_forward_dm256_kernel's layout) into a region; the
+  // reference exponents into wrr
+  auto ywrite = [&](char* region) {
+    const int ml = opaque(lane);
+    const int yt = ml >> 4;
+    constexpr float YS = 1.f / 2097152.f;            // 2^-21: |Y| <= n_in 2^9 < 65504 (n_in <= 127)
+    if (wave == 0 && (ml & 15) == 0) {
+      wrr[2 * yt] = rc[0];
+      wrr[2 * yt + 1] = rc[1];
+    }
+    uint32_t yh[BPW][2];
+#pragma unroll
+    for (int fb = 0; fb < BPW; ++fb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) yh[fb][s2] = pk_rne(acc[fb][2 * s2] * YS, acc[fb][2 * s2 + 1] * YS);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      char* yb = region + (2 * yt + s2) * SLOT + 16 * (ml & 15);
+      *reinterpret_cast<uint4*>(yb + yunit(0, wave, 0, 0)) = make_uint4(yh[0][s2], yh[4][s2], yh[8][s2], yh[12][s2]);
+      *reinterpret_cast<uint4*>(yb + yunit(0, wave, 0, 1)) = make_uint4(yh[2][s2], yh[6][s2], yh[10][s2], yh[14][s2]);
+      *reinterpret_cast<uint4*>(yb + yunit(1, wave, 0, 0)) = make_uint4(yh[1][s2], yh[5][s2], yh[9][s2], yh[13][s2]);
+      *reinterpret_cast<uint4*>(yb + yunit(1, wave, 0, 1)) = make_uint4(yh[3][s2], yh[7][s2], yh[11][s2], yh[15][s2]);
+    }
+#pragma unroll
+    for (int fb = 0; fb < BPW; ++fb) acc[fb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  // ---- stage 3 (wave w, token slot w): bc_forward_dm256_kernel's, with the token's reference
+  // exponent rref; tok < 0 stores nothing (the stores are still issued, with an empty range)
+  auto stage3 = [&](char* region, int rref, int64_t tok) {
+    const int l = opaque(lane);
+    const int o16 = l & 15, g = l >> 4;
+    char* slot = region + wave * SLOT;
+    const float ysc = __builtin_ldexpf(reinterpret_cast<const float*>(lds + OS2_OFF)[o16], 30 - rref);
+    uint4 ye[2][2], yz[2][2], yw[2][2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        ye[ks][pr] = *reinterpret_cast<const uint4*>(slot + yunit(0, 4 * ks + g, o16, pr));
+        yz[ks][pr] = *reinterpret_cast<const uint4*>(slot + yunit(1, 4 * ks + g, o16, pr));
+      }
+    const int gx = g ^ fsw(o16);
+    const char* gb = lds + F_OFF + 256 * o16;
+    auto gload = [&](int mt, f16x8 (&gf)[2][2]) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr)
+          gf[ks][pr] = *reinterpret_cast<const f16x8*>(gb + 4096 * mt + 16 * ((8 * pr + 4 * ks) ^ gx));
+    };
+    f16x8 gcur[2][2];
+    gload(0, gcur);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const uint4 z = yz[ks][pr];
+        yw[ks][pr] = make_uint4(__builtin_amdgcn_perm(z.x, z.x, 0x01000302u) ^ 0x80000000u,
+                                __builtin_amdgcn_perm(z.y, z.y, 0x01000302u) ^ 0x80000000u,
+                                __builtin_amdgcn_perm(z.z, z.z, 0x01000302u) ^ 0x80000000u,
+                                __builtin_amdgcn_perm(z.w, z.w, 0x01000302u) ^ 0x80000000u);
+      }
+    if (g == 0) {
+      yw[0][0].x = yz[0][0].x >> 16;
+      yz[0][0].x &= 0xffffu;
+    }
+    const bool tok_ok = tok >= 0 && tok < n_tokens;
+    const int nvalid = n_out - grp_o * NOB;
+    const int sw = 2 * o16;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      f32x4 E[3], O[3];
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        E[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+        O[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        E[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][0], __builtin_bit_cast(f16x8, ye[ks][0]), E[0], 0, 0, 0);
+        O[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][1], __builtin_bit_cast(f16x8, ye[ks][1]), O[0], 0, 0, 0);
+        E[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][0], __builtin_bit_cast(f16x8, yz[ks][0]), E[1], 0, 0, 0);
+        O[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][1], __builtin_bit_cast(f16x8, yz[ks][1]), O[1], 0, 0, 0);
+        E[2] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][0], __builtin_bit_cast(f16x8, yw[ks][0]), E[2], 0, 0, 0);
+        O[2] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][1], __builtin_bit_cast(f16x8, yw[ks][1]), O[2], 0, 0, 0);
+      }
+      if (mt < 3) gload(mt + 1, gcur);
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const float4 c01 = *reinterpret_cast<const float4*>(cs_l + 16 * mt + 4 * g + 64 * hf);
+        const float4 c23 = *reinterpret_cast<const float4*>(cs_l + 16 * mt + 4 * g + 64 * hf + 2);
+        const float cc[4] = {c01.x, c01.z, c23.x, c23.z}, ss[4] = {c01.y, c01.w, c23.y, c23.w};
+        float lo[4], hi[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = hf ? E[0][r] - O[0][r] : E[0][r] + O[0][r];
+          const float w = hf ? E[1][r] - O[1][r] : E[1][r] + O[1][r];
+          const float wp = hf ? E[2][r] - O[2][r] : E[2][r] + O[2][r];
+          const float o = fmaf(cc[r], w, -ss[r] * wp);
+          lo[r] = (e + o) * ysc;
+          hi[r] = (e - o) * ysc;
+        }
+        if (bias_dt != BCFFT_NONE) {                // .to(x dtype) :266, + bias :270-271
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            lo[r] = round_to(lo[r], XT);
+            hi[r] = round_to(hi[r], XT);
+          }
+          if (o16 < nvalid) {
+            const int64_t cc0 = (int64_t)(grp_o * NOB + o16) * B + 16 * mt + 4 * g + 64 * hf;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              lo[r] += load_scalar(bias, cc0 + r, bias_dt);
+              hi[r] += load_scalar(bias, cc0 + 128 + r, bias_dt);
+            }
+          }
+        }
+        const int u = 4 * mt + g + 16 * hf;
+        *reinterpret_cast<uint2*>(slot + 512 * o16 + 8 * (u ^ sw)) = make_uint2(pack16<XT>(lo[0], lo[1]), pack16<XT>(lo[2], lo[3]));
+        *reinterpret_cast<uint2*>(slot + 512 * o16 + 8 * ((u + 32) ^ sw)) = make_uint2(pack16<XT>(hi[0], hi[1]), pack16<XT>(hi[2], hi[3]));
+      }
+    }
+    constexpr int RB = B * ESY;
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (char*)yv + (tok_ok ? tok : 0) * M * ESY + (int64_t)grp_o * NOB * RB, 0,
+        tok_ok ? (int)((M - (int64_t)grp_o * NOB * B) * ESY) : 0, 0x00020000);
+    const int w = l & 31, lr = l >> 5;
+    uint4 dd[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int row = 2 * q + lr;
+      dd[q] = *reinterpret_cast<const uint4*>(slot + 512 * row + 16 * (w ^ row));
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dd[q]), yrs, (2 * q + lr) * RB + 16 * w, 0, 0);
+  };
+
+  // Pipeline: one step per (M-tile m of 8 tokens, chunk c), two barriers per step (rsel: the
+  // region holding chunk c's x; the other holds the previous chunk's X or, at c = 0, the
+  // previous tile's Y units):
+  //   c = 0   stage 3 of the previous tile's token w from the other region (8 stores)
+  //           x DMA of the next step's chunk into the other region (zeros past the last tile);
+  //           x(m, c) landed; stage 1                                                        | Ba |
+  //           stage 2 on B(c) (loaded in the previous step), loading the next step's B      | Bb |
+  //   c last  Y of the tile into this region                                                 | Be |
+  // VMEM younger than x(m, c) when it is waited for: B(c) 16 (the previous step's stage 2), at
+  // c = 0 the 8 stores, then the DMA (the first step's x and B were waited for in the prologue).
+  u32x4 breg[BPW];
+#pragma unroll
+  for (int fb = 0; fb < BPW; ++fb) load_b1(0, fb, breg);   // B(0), waited for by the prologue
+  wait_vmcnt<0>();
+  int rsel = 0;
+  int64_t mprev = -1;
+  int64_t m = wg_in_grp;
+  int c = 0;
+  while (m < n_mtiles) {
+    char* region = lds + rsel * REGION;
+    char* other = lds + (rsel ^ 1) * REGION;
+    const bool tile0 = c == 0;
+    if (tile0) {
+      stage3(other, wrr[wave], mprev >= 0 ? mprev * TT + wave : -1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
+    }
+    const bool last = c + 1 == nch;
+    const int64_t mn = last ? m + gstride : m;
+    const int cn = last ? 0 : c + 1;
+    dma_chunk(mn, cn, other);
+    if (tile0) wait_vmcnt<16 + 8 + NDMA_C>();
+    else wait_vmcnt<16 + NDMA_C>();
+    stage1(region);
+    lds_barrier();                                  // Ba: X units and chunk scales complete
+    stage2(region, breg, mn < n_mtiles ? cn : -1, tile0, tile0);
+    lds_barrier();                                  // Bb: every read of this chunk's X done
+    if (last) {
+      ywrite(region);
+      lds_barrier();                                // Be: Y units and reference exponents
+      mprev = m;
+    }
+    rsel ^= 1;
+    m = mn;
+    c = cn;
+  }
+  stage3(lds + (rsel ^ 1) * REGION, wrr[wave], mprev >= 0 ? mprev * TT + wave : -1);
 }
 
 // ---- weight image at b = 256: the generic STAT image kernels instantiated for B = 256 (groups
@@ -486,15 +1002,19 @@ bool dm256_eligible(int n_in, int b, int xdt, bool yf32) {
   return dm256_geometry(n_in, b) && xdt == BCFFT_BF16 && !yf32;
 }
 
-void launch_forward_dm256(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt,
-                          void* y, hipStream_t s) {
+void launch_forward_dm256(const void* x, int64_t n, int n_in, int n_out, const void* spec, const void* bias,
+                          int bias_dt, void* y, hipStream_t s) {
   const int groups = (n_out + d256::NOB - 1) / d256::NOB;
-  const SpecLayout sl = spec_layout(n_out, 16, 256);
+  const SpecLayout sl = spec_layout(n_out, n_in, 256);
   const int64_t n_mtiles = (n + 7) / 8;
   const int64_t total = group_grid(device_cu_count(), groups, n_mtiles);
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
   const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
-  hipLaunchKernelGGL(bc_forward_dm256_kernel, dim3((unsigned)total), dim3(512), 0, s, x, n, n_out, stat, osc, bias,
-                     bias_dt, y);
+  if (n_in == d256::NI)
+    hipLaunchKernelGGL(bc_forward_dm256_kernel, dim3((unsigned)total), dim3(512), 0, s, x, n, n_out, stat, osc, bias,
+                       bias_dt, y);
+  else
+    hipLaunchKernelGGL(bc_forward_dm256k_kernel, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat, osc,
+                       bias, bias_dt, y);
 }
 }  // namespace bcfft

@@ -846,7 +846,7 @@ int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_featur
     return record_launch();
   }
   if (algo == BCFFT_ALGO_DFT && dm256) {
-    bcfft::launch_forward_dm256(x, n_tokens, n_out, spectra, bias, bias_dtype, y, s);
+    bcfft::launch_forward_dm256(x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, s);
     return record_launch();
   }
   if (algo == BCFFT_ALGO_DFT && block_size == 64) {

@@ -1002,7 +1002,7 @@ template <int B>
 __global__ void bc_stat_image_kernel(int n_out, int n_in, float2* __restrict__ spec) {
   constexpr int H = B / 2, BW = H / 8, NT = 2, NW = 8;
   const SpecLayout sl = spec_layout(n_out, n_in, B);
-  const int ks_n = n_in / 16;
+  const int ks_n = (n_in + 15) / 16;
   const int npiece = sl.stat_pieces;
   const int64_t total = (int64_t)sl.stat_groups * NW * npiece * 64;
   uint32_t* hdr = reinterpret_cast<uint32_t*>(spec) + sl.stat_off_u32;

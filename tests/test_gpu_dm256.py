@@ -28,6 +28,16 @@ CASES = [
     (2048, 300, True),        # 8 output blocks: a partial group; several tiles per workgroup
     (4096, 2049, False),      # several tiles per workgroup on every CU
 ]
+# K != 4096 at b = 256: the streamed-weight chunk kernel (bc_forward_dm256k_kernel)
+CASES_K = [
+    # (K, M, N, bias)
+    (11008, 4096, 37, False),   # the down projection: 43 input blocks = 2 full chunks + 11
+    (11008, 4096, 1, True),     # one token, bf16 bias
+    (11008, 4096, 2049, False), # several tiles per workgroup
+    (8192, 2048, 300, True),    # 2 full chunks; 8 output blocks (a partial N-tile)
+    (2048, 4096, 19, False),    # K < 4096: one partial chunk (8 blocks)
+    (5120, 11008, 64, False),   # 20 input blocks, 3 N-tile groups
+]
 
 
 @pytest.mark.parametrize("m,n,bias", CASES)
@@ -48,6 +58,53 @@ def test_dm256_vs_oracle(dev, m, n, bias):
     g = y.float().cpu().numpy()
     for t in sorted({0, n // 2, n - 1}):
         assert rel_err(g[t], ref[t]) < 4e-3, (t, rel_err(g[t], ref[t]))
+
+
+@pytest.mark.parametrize("k,m,n,bias", CASES_K)
+def test_dm256k_vs_oracle(dev, k, m, n, bias):
+    b = 256
+    rng = np.random.default_rng(k + m + n)
+    c = (rng.standard_normal((m // b, k // b, b)) * 0.01).astype(np.float32)
+    bv = (rng.standard_normal(m) * 0.1).astype(np.float32) if bias else None
+    x = rng.standard_normal((n, k)).astype(np.float32)
+    y, ref = _run(dev, x, c, bv, "bfloat16", "bfloat16", algo="dft")
+    _check(y, ref, "bfloat16")
+    ya, _ = _run(dev, x, c, bv, "bfloat16", "bfloat16", algo="auto")
+    assert torch.equal(y, ya)
+    # per-(token, chunk) scales: a 300x token; a token whose first chunk is 1e-3-quiet and
+    # whose last is loud (the reference exponent drops: accumulator rows rescale); a token with
+    # one all-zero chunk
+    x[0] *= 300.0
+    x[n - 1, :4096] *= 1e-3
+    x[n - 1, -100:] *= 40.0
+    if n > 2 and k > 4096:
+        x[n // 2, 4096:8192] = 0.0
+    y, ref = _run(dev, x, c, bv, "bfloat16", "bfloat16", algo="dft")
+    g = y.float().cpu().numpy()
+    for t in sorted({0, n // 2, n - 1}):
+        assert rel_err(g[t], ref[t]) < 4e-3, (t, rel_err(g[t], ref[t]))
+
+
+def test_dm256k_full_size_down(dev):
+    """The block-size sweep's down projection at b = 256 (11008 -> 4096, N = 8192): every token
+    within ~1 bf16 ulp of the oracle, run-to-run bit equality."""
+    from bcfft import ops
+    from oracle import bc_oracle as O
+    k, m, b, n = 11008, 4096, 256, 8192
+    rng = np.random.default_rng(8)
+    c = O.round_to((rng.standard_normal((m // b, k // b, b)) * 0.01).astype(np.float32), O.BF16)
+    x = O.round_to(rng.standard_normal((n, k)).astype(np.float32), O.BF16)
+    spec = ops.spectra(torch.from_numpy(c).to(dev).to(torch.bfloat16))
+    xt = torch.from_numpy(x).to(dev).to(torch.bfloat16)
+    y = ops.forward(xt, spec, None, b, m, algo="auto")
+    assert torch.equal(y, ops.forward(xt, spec, None, b, m, algo="auto"))
+    g = y.float().cpu().numpy()
+    ref = O.bc_forward(x, c, None, x_dtype=O.BF16)
+    ulp = 2.0 ** -7
+    rms = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
+    bad = np.abs(g - ref) > 2 * ulp * np.abs(ref) + 2 * ulp * rms
+    assert not bad.any(), f"{int(bad.sum())} elements beyond ~1 ulp"
+    assert rel_err(g, ref) < 4e-3
 
 
 def test_dm256_full_size_sweep_shape(dev):

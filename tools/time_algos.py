@@ -75,6 +75,12 @@ if __name__ == "__main__":
         shapes = [(11008, 4096, 64, "bf16", n) for n in (1700, 8192)]
     if "--downsmall" in sys.argv:                   # decode sizes: AUTO's floor for the streamed kernel
         shapes = [(11008, 4096, 128, "bf16", n) for n in (1, 2, 4, 8, 16, 32)]
+    if "--pipe" in sys.argv:                        # the bf16 K = 4096 DFT kernels (dm8, dmg, dm256, dm64)
+        shapes = [(4096, 4096, 128, "bf16", 8192), (4096, 11008, 128, "bf16", 8192), (4096, 4096, 256, "bf16", 8192),
+                  (4096, 11008, 256, "bf16", 8192), (4096, 4096, 64, "bf16", 8192), (4096, 4096, 128, "bf16", 1024)]
+    if "--b256" in sys.argv:                        # the b = 256 sweep rows (bcfft_dm256.hip)
+        shapes = [(4096, 4096, 256, "bf16", 8192), (4096, 11008, 256, "bf16", 8192), (11008, 4096, 256, "bf16", 8192),
+                  (11008, 4096, 256, "bf16", 1024), (11008, 4096, 256, "bf16", 64)]
     if "--down2" in sys.argv:
         shapes = [(11008, 4096, 128, "bf16", n) for n in (1700, 8192)]
     if "--smalln" in sys.argv:                      # AUTO's small-N crossover
