@@ -60,6 +60,10 @@ def resolved_kernel(algo, k, b, io="fp32", m=4096):
         algo = "dftx"
     stat_ok = (b == 128 and n_in == 32) or (b == 64 and n_in in (32, 64))
     dft_ok = b == 128 and n_in == 32
+    if io == "bf16" and algo in ("dft", "auto") and b == 64 and 64 < n_in <= 255:
+        return ("dft", "bc_forward_dm64k_kernel",
+                "MFMA fp16 throughout, b=64, 16 tokens per tile, 32-block K-chunks with weight fragments "
+                "streamed from L2 (bf16 I/O)")
     if io == "bf16" and algo in ("dft", "auto") and b == 64 and n_in == 64:
         return ("dft", "bc_forward_dm64_kernel",
                 "MFMA fp16 throughout, b=64, 8 tokens per tile, one-term spectra (bf16 I/O)")

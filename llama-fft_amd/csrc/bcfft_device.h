@@ -505,6 +505,9 @@ constexpr int STAT_OUT_BLOCKS = 32;    // output blocks per stationary group (tw
 // image's (ceil(n_in / 16) K-steps, 16 bins per wave); a workgroup takes one N-tile (16 output
 // blocks) of a group. n_in <= 127 keeps Y = acc 2^-21 below fp16's max.
 __host__ __device__ inline bool dm256_geometry(int n_in, int b) { return b == 256 && n_in >= 1 && n_in <= 127; }
+// the b = 64 streamed-weight DFT kernel (bcfft_dm64k.hip): K > 4096, 32-block chunks of the STAT
+// image's K-steps (ceil(n_in / 16)); n_in <= 255 keeps Y = acc 2^-21 below fp16's max at b = 64
+__host__ __device__ inline bool dm64k_geometry(int n_in, int b) { return b == 64 && n_in > 64 && n_in <= 255; }
 // streamed-weight DFT kernel geometries (bcfft_dmk.hip): b = 128 with K > 4096. The same 16-B
 // header, then per output group of 32 blocks, per 16-block K-chunk, per wave (4), per bin of
 // the wave (16), per N-tile (2), per lane: the fp16 B fragment the lane loads for that chunk
@@ -528,7 +531,7 @@ __host__ __device__ inline SpecLayout spec_layout(int n_out, int n_in, int b) {
     s.img_u32 = 0;
   }
   s.stat_off_u32 = s.img_off_u32 + s.img_u32;
-  if (stat_eligible(n_in, b) || dm256_geometry(n_in, b)) {
+  if (stat_eligible(n_in, b) || dm256_geometry(n_in, b) || dm64k_geometry(n_in, b)) {
     s.stat_groups = (n_out + STAT_OUT_BLOCKS - 1) / STAT_OUT_BLOCKS;
     s.stat_pieces = (h / 8) * ((n_in + 15) / 16) * 2;   // bins/wave x K-steps x N-tiles
     s.stat_u32 = 4 + (int64_t)s.stat_groups * 8 * s.stat_pieces * 64 * 4;
@@ -576,6 +579,13 @@ void launch_forward_dm8(const void* x, int64_t n, int n_out, const void* spec, c
 // b = 256, n_in <= 127, bf16 x and bf16 y (no bias or a bf16 bias) (bcfft_dm256.hip)
 bool dm256_eligible(int n_in, int b, int xdt, bool yf32);
 void launch_forward_dm256(const void* x, int64_t n, int n_in, int n_out, const void* spec, const void* bias,
+                          int bias_dt, void* y, hipStream_t s);
+// b = 64, K > 4096 (up to 255 input blocks), bf16 x and bf16 y (bcfft_dm64k.hip)
+bool dm64k_eligible(int n_in, int b, int xdt, bool yf32);
+#ifndef BCFFT_DM64K_MIN_TOKENS
+#define BCFFT_DM64K_MIN_TOKENS 128   // AUTO picks the b = 64 streamed-weight kernel from this many tokens
+#endif
+void launch_forward_dm64k(const void* x, int64_t n, int n_in, int n_out, const void* spec, const void* bias,
                           int bias_dt, void* y, hipStream_t s);
 // streamed-weight DFT kernel (bcfft_dmk.hip): b = 128, K > 4096, bf16 x and bf16 y
 bool dmk_eligible(int n_in, int b, int xdt, bool yf32);

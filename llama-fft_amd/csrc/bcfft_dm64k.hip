@@ -1,0 +1,528 @@
+// bcfft_dm64k.hip — the DFT-on-MFMA block-circulant forward at b = 64 for K > 4096, bf16 I/O
+// (gfx950): the LLaMA down projection 11008 -> 4096 at b = 64 (172 input blocks) and every other
+// wide-input layer at that block size.
+//
+// Same operator (BlockCirculantLinear.forward, patch_llama_fft.py:226-275; per block
+// src/fft_utils.py:3-34) and the same three matrix-core stages as bcfft_dm64.hip. An output
+// group's fp16 spectra at K = 11008 (32 x 172 blocks x 32 bins x 4 B = 704 KiB) do not fit the
+// register file, so the K axis is cut into 32-block chunks (two 16-block K-steps) and each
+// chunk's B fragments (16 per wave: 4 bins x 2 K-steps x 2 N-tiles, 64 VGPRs) are streamed from
+// L2 once per 16-token tile, the next step's fragment of a bin loaded into its registers as soon
+// as the bin's MFMAs are issued. Per-bin products accumulate in 64 fp32 VGPRs over all chunks.
+//
+//  * Workgroup: 8 waves, persistent, one per CU; wave w owns tokens w and w + 8 of the tile for
+//    the x DMA, stage 1 and stage 3 (so no barrier is needed between its stage 3 and the DMA
+//    into the same slots), and bins 4w .. 4w + 3 in stage 2 for all 16 tokens.
+//  * One step per (tile, chunk): [tile's first chunk: stage 3 of the previous tile's tokens w,
+//    w + 8] -> x DMA of the next step's chunk into the other region -> stage 1 | Ba | stage 2 |
+//    Bb | [last chunk: Y of the 16 tokens into the chunk's region | Be].
+//  * Numerics: per-(token, 16-block quarter) power-of-two scales from stage 1 with HEAD bits of
+//    headroom; stage 2 aligns each quarter to the token's running reference exponent (an exact
+//    fp16 power of two on the A rows) and scales the accumulator rows down once when a chunk is
+//    more than 2^HEAD louder (bcfft_dmk.hip's scheme). |X| <= 2^(13 - HEAD) at b = 64, so
+//    Y = acc 2^-21 <= n_in 2^8 stays below fp16's max for n_in <= 255.
+//
+// LDS (138,816 B): two regions x 16 token slots of 4,160 B (a token's 32-block x chunk, 32 rows x
+// 128 B -> X units (2 K-steps x 2 KiB, bcfft_dm64.hip's map) -> at the tile end Y half-units ->
+// y staging), the 4 KiB DFT table, the scales.
+#include "bcfft_device.h"
+#include "bcfft_dm_table.h"
+#include "bcfft_dm_common.h"
+
+namespace bcfft {
+
+namespace dm64k {
+using namespace dmh;
+
+constexpr int B = 64, NW = 8, TT = 16, MT = 2, BW = 4, NT = 2, KC = 2, NOG = 32;
+constexpr int XSLOT = 4096 + 64;                    // one token's chunk (32 blocks x 128 B)
+constexpr int REGION = TT * XSLOT;
+constexpr int F_OFF = 2 * REGION;                   // DFT table image, 32 rows x 128 B
+constexpr int SC_OFF = F_OFF + 4096;                // scale exponents [16 tokens][2 quarters]
+constexpr int RR_OFF = SC_OFF + 128;                // per-token reference exponents [16]
+constexpr int OS_OFF = RR_OFF + 64;                 // the group's 32 inverse weight scales
+constexpr int LDS_BYTES = OS_OFF + 128;
+constexpr int FRAGS = BW * KC * NT;                 // B fragments per wave and chunk
+constexpr int NDMA = 2 * 4;                         // 1-KiB x DMA pieces per wave and chunk (2 tokens)
+constexpr int HEAD = 4;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+static_assert(XSLOT % 256 == 64, "slot stride 64 B off the bank period");
+
+__device__ __forceinline__ int fsw64(int t) { return (((t >> 1) & 1) << 1) | (((t >> 3) & 1) << 2); }
+__device__ __forceinline__ int yhalf64(int w, int o, int par) { return 2048 * par + 256 * w + 8 * (o ^ (16 * ((w >> 1) & 1))); }
+// fp16 factor 2^-d (d >= -15) as a (lo, hi) pair: subnormal below 2^-14, zero below 2^-24
+__device__ __forceinline__ uint32_t f16_pow2_neg(int d) {
+  return d <= 14 ? (uint32_t)(15 - d) << 10 : (d <= 24 ? 1u << (24 - d) : 0u);
+}
+}  // namespace dm64k
+
+__global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
+    const void* __restrict__ xv, int64_t n_tokens, int n_in, int n_out, const uint32_t* __restrict__ stat,
+    const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
+  using namespace dm64k;
+  constexpr int XT = BCFFT_BF16;
+  constexpr int ES = 2, ESY = 2;
+
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  int* wsc = reinterpret_cast<int*>(lds + SC_OFF);
+  int* wrr = reinterpret_cast<int*>(lds + RR_OFF);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n_groups = (n_out + NOG - 1) / NOG;
+  const GroupMap gm = group_map(n_groups);
+  const int grp_o = gm.grp, wg_in_grp = gm.lane;
+  const int64_t KX = (int64_t)n_in * B;
+  const int64_t M = (int64_t)n_out * B;
+  const int nch = (n_in + 31) / 32;
+  const int KS = (n_in + 15) / 16;                  // K-steps of the STAT image
+  const int64_t n_mtiles = (n_tokens + TT - 1) / TT;
+  const int gstride = gm.stride;
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+
+  // ---- chunk c of tokens w and w + 8 of M-tile m -> their slots by LDS-DMA: piece q = rows
+  // 8q + (lane >> 3) of 128 B, unit u of row r at u ^ (r & 7); the buffer range ends at the row
+  // end, so a partial last chunk and tokens / tiles past the end land as zeros
+  auto dma_chunk = [&](int64_t m, int c, char* region) {
+    const int dl = opaque(lane);
+    const int r = dl >> 3;
+    const int vb = r * 128 + 16 * ((dl & 7) ^ r);
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {
+      const int tl = wave + 8 * t2;
+      const int64_t tok = m * TT + tl;
+      const bool ok = m < n_mtiles && tok < n_tokens;
+      const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<char*>((const char*)xv) + (ok ? tok * KX * ES + (int64_t)c * 4096 : 0), 0,
+          ok ? (int)(KX * ES - (int64_t)c * 4096) : 0, 0x00020000);
+      const uint32_t dst0 = lds_base + (uint32_t)(region - lds) + tl * XSLOT;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(vb), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
+      }
+    }
+  };
+
+  // ---- B fragments (STAT image group grp_o, wave, piece (fb KS + 2c + j) 2 + nt), asm loads
+  // counted by hand (bcfft_dmk.hip's scheme): wait_b is their one wait, with the exact number of
+  // younger VMEM operations, and it redefines the registers it waited for
+  const int npiece = BW * KS * NT;
+  const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint32_t*>(stat + 4) + ((int64_t)(grp_o * NW + wave) * npiece) * 256, 0, npiece * 1024, 0x00020000);
+  // fragment (fb, j, nt) of chunk c; K-step 2c + 1 past the image (odd KS, last chunk) reads zeros
+  auto load_b1 = [&](int c, int fb, int j, int nt, u32x4 (&breg)[BW][KC][NT]) {
+    const int ks = 2 * c + j;
+    const int vo = opaque(lane) * 16 + (ks < KS ? (fb * KS + ks) * 2 + nt : npiece) * 1024;
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(breg[fb][j][nt]) : "v"(vo), "s"(brs));
+  };
+  auto wait_b = [&](auto n_tag, u32x4 (&breg)[BW][KC][NT]) {
+    constexpr int N = decltype(n_tag)::value;
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    asm volatile("s_waitcnt vmcnt(%16)"
+                 : "+v"(breg[0][0][0]), "+v"(breg[0][0][1]), "+v"(breg[0][1][0]), "+v"(breg[0][1][1]),
+                   "+v"(breg[1][0][0]), "+v"(breg[1][0][1]), "+v"(breg[1][1][0]), "+v"(breg[1][1][1]),
+                   "+v"(breg[2][0][0]), "+v"(breg[2][0][1]), "+v"(breg[2][1][0]), "+v"(breg[2][1][1]),
+                   "+v"(breg[3][0][0]), "+v"(breg[3][0][1]), "+v"(breg[3][1][0]), "+v"(breg[3][1][1])
+                 : "n"(N) : "memory");
+  };
+  static_assert(FRAGS == 16, "wait_b names sixteen fragments");
+
+  // ---- prologue: the first tile's chunk 0, the DFT table, the inverse weight scales
+  dma_chunk(wg_in_grp, 0, lds);
+  if (tid < 256) {                                  // chunk c: row c >> 3, chunk c & 7
+    const uint4* tab = reinterpret_cast<const uint4*>(kDmF64);
+    const int t = tid >> 3, ch = tid & 7;
+    *reinterpret_cast<uint4*>(lds + F_OFF + 128 * t + 16 * (ch ^ fsw64(t))) = tab[tid];
+  }
+  if (tid < 32) reinterpret_cast<float*>(lds + OS_OFF)[tid] = osc[grp_o * 32 + tid];
+  wait_vmcnt<0>();
+  lds_barrier();
+
+  // ---- stage 1 (wave w: tokens w, w + 8): bcfft_dm64.hip's stage 1 on the chunk's two quarters,
+  // the scale of each lowered by HEAD bits
+  auto stage1 = [&](char* region) {
+    const int l = opaque(lane);
+    const int b16 = l & 15, g = l >> 4;
+    const int q4 = (l & 15) >> 2, p4 = l & 3;
+    const int r0 = 8 * g + q4, r1 = r0 + 4;
+    const int trb0 = F_OFF + 128 * r0 + 8 * (p4 & 1), trb1 = F_OFF + 128 * r1 + 8 * (p4 & 1);
+    const int cx0 = (p4 >> 1) ^ fsw64(r0), cx1 = (p4 >> 1) ^ fsw64(r1);
+    int xwb[2];
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) xwb[pr] = 256 * g + 64 * (pr ^ (g & 1)) + 4 * b16;
+#pragma unroll 1
+    for (int t2 = 0; t2 < 2; ++t2) {
+      const int tl = wave + 8 * t2;
+      char* slot = region + tl * XSLOT;
+#pragma unroll
+      for (int h = 0; h < KC; ++h) {
+        float xq[2][8];
+        const char* rowp = slot + (16 * h + b16) * (B * ES);
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt) {
+          const uint4 w = *reinterpret_cast<const uint4*>(rowp + 16 * ((g + 4 * pt) ^ (b16 & 7)));
+          const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float2 f = unpack16<XT>(ww[e]);
+            xq[pt][2 * e] = f.x;
+            xq[pt][2 * e + 1] = f.y;
+          }
+        }
+        float m0 = 0.f, m1 = 0.f;
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+          for (int j = 0; j < 8; j += 4) {
+            m0 = amax3(m0, xq[pt][j], xq[pt][j + 1]);
+            m1 = amax3(m1, xq[pt][j + 2], xq[pt][j + 3]);
+          }
+        const float mxf = __builtin_fmaxf(m0, m1);
+        const int sx = stat_scale_exp(2.f * __uint_as_float(wave_umax(__float_as_uint(mxf)))) - HEAD;
+        if (l == 0) wsc[tl * 2 + h] = sx - 7;      // X = D 2^-(sx - 7): the table's 2^-7
+        const float S = __int_as_float((sx + 127) << 23);
+        uint32_t ah[4], dh[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float u0 = xq[1][2 * e] * S, u1 = xq[1][2 * e + 1] * S;
+          ah[e] = pk_rne(fmaf(xq[0][2 * e], S, u0), fmaf(xq[0][2 * e + 1], S, u1));
+          dh[e] = pk_rne(fmaf(xq[0][2 * e], S, -u0), fmaf(xq[0][2 * e + 1], S, -u1));
+        }
+        const f16x8 bah = frag(ah[0], ah[1], ah[2], ah[3]), bdh = frag(dh[0], dh[1], dh[2], dh[3]);
+        f32x4 acc4[4];
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) {
+            const int c = 4 * pr + 2 * mt;
+            const s16x4 ra = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) s16x4*)(lds + trb0 + 16 * (c ^ cx0)));
+            const s16x4 rb = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) s16x4*)(lds + trb1 + 16 * (c ^ cx1)));
+            const f16x8 af = __builtin_bit_cast(f16x8, __builtin_shufflevector(ra, rb, 0, 1, 2, 3, 4, 5, 6, 7));
+            acc4[2 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, pr ? bdh : bah, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          }
+        char* xb = slot + 2048 * h;
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) {
+            *reinterpret_cast<uint32_t*>(xb + xwb[pr] + 1024 * mt) = pk_rne(acc4[2 * pr + mt][0], acc4[2 * pr + mt][1]);
+            *reinterpret_cast<uint32_t*>(xb + xwb[pr] + 1024 * mt + 128) = pk_rne(acc4[2 * pr + mt][2], acc4[2 * pr + mt][3]);
+          }
+      }
+    }
+  };
+
+  // accumulators [bin of the wave][M-tile][N-tile]: rows 4 yt + r = token 8 mt + 2 yt + (r >> 1),
+  // re / im r & 1; reference exponents of the A-row tokens and the accumulator-row tokens
+  f32x4 acc[BW][MT][NT];
+#pragma unroll
+  for (int fb = 0; fb < BW; ++fb)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[fb][mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int ra[MT] = {0, 0};
+  int rc[MT][2] = {{0, 0}, {0, 0}};
+
+  // ---- stage 2 (all waves): the chunk's per-bin complex MAC on bins 4 wave + fb for the 16
+  // tokens, accumulated; each fragment's successor for the next step (nb >= 0) is loaded into
+  // its registers after its last MFMA. One call site.
+  auto stage2 = [&](char* region, u32x4 (&breg)[BW][KC][NT], int nb, bool first, bool tile0) {
+    const int ml = opaque(lane);
+    const int arow = ml & 15, kb = ml >> 4;
+    const int a_t = arow >> 1, a_reim = arow & 1;
+    const uint32_t a_sel = a_reim ? 0x01000302u : 0x03020100u;
+    const int yt = ml >> 4;
+    int nk[MT][KC];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int j = 0; j < KC; ++j) nk[mt][j] = wsc[(8 * mt + a_t) * 2 + j];
+    if (first) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        ra[mt] = min(nk[mt][0], nk[mt][1]);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int* sc = wsc + (8 * mt + 2 * yt + s) * 2;
+          rc[mt][s] = min(sc[0], sc[1]);
+        }
+      }
+    } else {
+      float fct[MT][2];
+      bool need = false;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        ra[mt] = min(ra[mt], min(nk[mt][0], nk[mt][1]) + HEAD);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int* sc = wsc + (8 * mt + 2 * yt + s) * 2;
+          const int nn = min(sc[0], sc[1]) + HEAD;
+          const int d = rc[mt][s] - nn;
+          fct[mt][s] = d > 0 ? __builtin_ldexpf(1.f, -d) : 1.f;
+          need |= d > 0;
+          rc[mt][s] = min(rc[mt][s], nn);
+        }
+      }
+      if (__builtin_amdgcn_ballot_w64(need)) {
+#pragma unroll
+        for (int fb = 0; fb < BW; ++fb)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) acc[fb][mt][nt][r] *= fct[mt][r >> 1];
+      }
+    }
+    uint32_t amul[MT][KC], amul0[MT][KC];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int j = 0; j < KC; ++j) {
+        const int d = nk[mt][j] - ra[mt];           // >= -HEAD: factor 2^-d <= 2^HEAD
+        const uint32_t hh = f16_pow2_neg(d);
+        const uint32_t h0 = f16_pow2_neg(d + 1);    // bin 0: the inverse's 1/b vs 2/b
+        amul[mt][j] = a_reim ? (hh | ((hh | 0x8000u) << 16)) : (hh | (hh << 16));
+        amul0[mt][j] = a_reim ? (h0 << 16) : h0;
+      }
+    const int sw = 64 * (wave & 1);
+    // B of this step: younger VMEM is this step's x DMA and, at a tile's first chunk, the
+    // previous tile's stage-3 stores before it
+    if (tile0) wait_b(std::integral_constant<int, 8 + NDMA>{}, breg);
+    else wait_b(std::integral_constant<int, NDMA>{}, breg);
+    const int nc = nb < 0 ? 0 : nb;
+#pragma unroll
+    for (int fb = 0; fb < BW; ++fb) {
+      const int f = wave * BW + fb;
+#pragma unroll
+      for (int j = 0; j < KC; ++j) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const char* ab = region + (8 * mt + a_t) * XSLOT + 256 * wave + 16 * kb + ((fb & 1) ? -sw : sw) + 64 * fb + 2048 * j;
+          uint4 raw = *reinterpret_cast<const uint4*>(ab);
+          if (f == 0) {
+            raw.x = pkmul(raw.x, amul0[mt][j]); raw.y = pkmul(raw.y, amul0[mt][j]);
+            raw.z = pkmul(raw.z, amul0[mt][j]); raw.w = pkmul(raw.w, amul0[mt][j]);
+          } else {
+            raw.x = pkmul(__builtin_amdgcn_perm(raw.x, raw.x, a_sel), amul[mt][j]);
+            raw.y = pkmul(__builtin_amdgcn_perm(raw.y, raw.y, a_sel), amul[mt][j]);
+            raw.z = pkmul(__builtin_amdgcn_perm(raw.z, raw.z, a_sel), amul[mt][j]);
+            raw.w = pkmul(__builtin_amdgcn_perm(raw.w, raw.w, a_sel), amul[mt][j]);
+          }
+          const f16x8 a = __builtin_bit_cast(f16x8, raw);
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            acc[fb][mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, __builtin_bit_cast(f16x8, breg[fb][j][nt]),
+                                                                     acc[fb][mt][nt], 0, 0, 0);
+        }
+        if (nb >= 0) {
+          load_b1(nc, fb, j, 0, breg);
+          load_b1(nc, fb, j, 1, breg);
+        }
+      }
+    }
+  };
+
+  // ---- Y of the 16 tokens (fp16 half-units, bcfft_dm64.hip's map) into their slots of a
+  // region; the reference exponents into wrr; the accumulators restart at zero
+  auto ywrite = [&](char* region) {
+    const int ml = opaque(lane);
+    const int yt = ml >> 4;
+    constexpr float YS = 1.f / 2097152.f;            // 2^-21: |Y| <= n_in 2^8 < 65504 (n_in <= 255)
+    if (wave == 0 && (ml & 15) == 0) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        wrr[8 * mt + 2 * yt] = rc[mt][0];
+        wrr[8 * mt + 2 * yt + 1] = rc[mt][1];
+      }
+    }
+    const int ox = 16 * ((wave >> 1) & 1);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      uint32_t yh[BW][NT][2];
+#pragma unroll
+      for (int fb = 0; fb < BW; ++fb)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+            yh[fb][nt][s2] = pk_rne(acc[fb][mt][nt][2 * s2] * YS, acc[fb][mt][nt][2 * s2 + 1] * YS);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        char* yb = region + (8 * mt + 2 * yt + s2) * XSLOT + 256 * wave;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {           // yhalf64(wave, 16 nt + o16, par)
+          const int oo = 8 * ((16 * nt + (ml & 15)) ^ ox);
+          *reinterpret_cast<uint2*>(yb + oo) = make_uint2(yh[0][nt][s2], yh[2][nt][s2]);
+          *reinterpret_cast<uint2*>(yb + 2048 + oo) = make_uint2(yh[1][nt][s2], yh[3][nt][s2]);
+        }
+      }
+    }
+#pragma unroll
+    for (int fb = 0; fb < BW; ++fb)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[fb][mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  // ---- stage 3 (token slot tl of a region, reference exponent rref): bcfft_dm64.hip's stage 3;
+  // tok < 0 stores nothing (the stores are still issued, with an empty range)
+  auto stage3 = [&](char* region, int tl, int rref, int64_t tok) {
+    const int l = opaque(lane);
+    const int o16 = l & 15, g = l >> 4;
+    char* slot = region + tl * XSLOT;
+    float ysc[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) ysc[nt] = __builtin_ldexpf(reinterpret_cast<const float*>(lds + OS_OFF)[16 * nt + o16], 30 - rref);
+    uint4 yf[2][NT];
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int o = 16 * nt + o16;
+        const uint2 lo = *reinterpret_cast<const uint2*>(slot + yhalf64(2 * g, o, pr));
+        const uint2 hi = *reinterpret_cast<const uint2*>(slot + yhalf64(2 * g + 1, o, pr));
+        yf[pr][nt] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+    f16x8 gt[2][2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const int t = 16 * mt + o16;
+        gt[mt][pr] = *reinterpret_cast<const f16x8*>(lds + F_OFF + 128 * t + 16 * ((4 * pr + g) ^ fsw64(t)));
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // Y is in registers: the slot is free
+    const bool tok_ok = tok >= 0 && tok < n_tokens;
+    const int nvalid = n_out - grp_o * NOG;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      f32x4 E[NT], O[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        E[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gt[mt][0], __builtin_bit_cast(f16x8, yf[0][nt]), f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        O[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gt[mt][1], __builtin_bit_cast(f16x8, yf[1][nt]), f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int o = 16 * nt + o16;
+        float os[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) os[r] = O[nt][r] * ysc[nt];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = hf ? fmaf(E[nt][r], ysc[nt], -os[r]) : fmaf(E[nt][r], ysc[nt], os[r]);
+          if (bias_dt != BCFFT_NONE) {              // .to(x dtype) :266, + bias :270-271
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = round_to(v[r], XT);
+            if (o < nvalid) {
+              const int64_t cc = (int64_t)(grp_o * NOG + o) * B + 16 * mt + 4 * g + 32 * hf;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] += load_scalar(bias, cc + r, bias_dt);
+            }
+          }
+          *reinterpret_cast<uint2*>(slot + 128 * o + 8 * ((4 * mt + g + 8 * hf) ^ o16)) =
+              make_uint2(pack16<XT>(v[0], v[1]), pack16<XT>(v[2], v[3]));
+        }
+      }
+    }
+    constexpr int RB = B * ESY;
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (char*)yv + (tok_ok ? tok : 0) * M * ESY + (int64_t)grp_o * NOG * RB, 0,
+        tok_ok ? (int)((M - (int64_t)grp_o * NOG * B) * ESY) : 0, 0x00020000);
+    const int w = l & 7, lr = l >> 3;
+    const int vofs = lr * RB + 16 * w;
+    uint4 d[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rr = 8 * q + lr;
+      uint4 v = *reinterpret_cast<const uint4*>(slot + 128 * rr + 16 * (w ^ ((rr & 15) >> 1)));
+      if (lr & 1) v = make_uint4(v.z, v.w, v.x, v.y);
+      d[q] = v;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs, vofs + q * 1024, 0, 0);
+  };
+
+  // Pipeline: one step per (M-tile m of 16 tokens, chunk c), two barriers per step (rsel: the
+  // region holding chunk c's x; the other holds the previous chunk's X or, at c = 0, the
+  // previous tile's Y units):
+  //   c = 0   stage 3 of the previous tile's tokens w, w + 8 from the other region (8 stores)
+  //           x DMA of the next step's chunk into the other region (zeros past the last tile);
+  //           x(m, c) landed; stage 1                                                        | Ba |
+  //           stage 2 on B(c) (loaded in the previous step), loading the next step's B      | Bb |
+  //   c last  Y of the tile into this region                                                 | Be |
+  // VMEM younger than x(m, c) when it is waited for: B(c) 16 (the previous step's stage 2), at
+  // c = 0 the 8 stores, then the DMA (the first step's x and B were waited for up front).
+  u32x4 breg[BW][KC][NT];
+#pragma unroll
+  for (int fb = 0; fb < BW; ++fb)
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      load_b1(0, fb, j, 0, breg);
+      load_b1(0, fb, j, 1, breg);
+    }
+  wait_vmcnt<0>();
+  int rsel = 0;
+  int64_t mprev = -1;
+  int64_t m = wg_in_grp;
+  int c = 0;
+  while (m < n_mtiles) {
+    char* region = lds + rsel * REGION;
+    char* other = lds + (rsel ^ 1) * REGION;
+    const bool tile0 = c == 0;
+    if (tile0) {
+      stage3(other, wave, wrr[wave], mprev >= 0 ? mprev * TT + wave : -1);
+      stage3(other, wave + 8, wrr[wave + 8], mprev >= 0 ? mprev * TT + wave + 8 : -1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slots' staging reads are done
+    }
+    const bool last = c + 1 == nch;
+    const int64_t mn = last ? m + gstride : m;
+    const int cn = last ? 0 : c + 1;
+    dma_chunk(mn, cn, other);
+    if (tile0) wait_vmcnt<FRAGS + 8 + NDMA>();
+    else wait_vmcnt<FRAGS + NDMA>();
+    stage1(region);
+    lds_barrier();                                  // Ba: X units and quarter scales complete
+    stage2(region, breg, mn < n_mtiles ? cn : -1, tile0, tile0);
+    lds_barrier();                                  // Bb: every read of this chunk's X done
+    if (last) {
+      ywrite(region);
+      lds_barrier();                                // Be: Y units and reference exponents
+      mprev = m;
+    }
+    rsel ^= 1;
+    m = mn;
+    c = cn;
+  }
+  char* yreg = lds + (rsel ^ 1) * REGION;
+  stage3(yreg, wave, wrr[wave], mprev >= 0 ? mprev * TT + wave : -1);
+  stage3(yreg, wave + 8, wrr[wave + 8], mprev >= 0 ? mprev * TT + wave + 8 : -1);
+}
+
+bool dm64k_eligible(int n_in, int b, int xdt, bool yf32) {
+  return dm64k_geometry(n_in, b) && xdt == BCFFT_BF16 && !yf32;
+}
+
+void launch_forward_dm64k(const void* x, int64_t n, int n_in, int n_out, const void* spec, const void* bias,
+                          int bias_dt, void* y, hipStream_t s) {
+  const int groups = (n_out + dm64k::NOG - 1) / dm64k::NOG;
+  const SpecLayout sl = spec_layout(n_out, n_in, 64);
+  const int64_t n_mtiles = (n + dm64k::TT - 1) / dm64k::TT;
+  const int64_t total = group_grid(device_cu_count(), groups, n_mtiles);
+  const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
+  const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
+  hipLaunchKernelGGL(bc_forward_dm64k_kernel, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat, osc,
+                     bias, bias_dt, y);
+}
+
+}  // namespace bcfft

@@ -75,6 +75,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
   const int64_t n_mtiles = (n_tokens + TT - 1) / TT;
   const int gstride = gm.stride;
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+#ifdef BCFFT_STAMPS
+  ANALYSIS_INIT;
+  (void)ablate_flags_;
+#endif
 
   // ---- x of token `wave` of M-tile m -> its slot by LDS-DMA (the buffer range zero-fills
   // tokens past n_tokens); piece q = rows 4q + (lane >> 4), 256 B each, with the slot's unit
@@ -437,25 +441,34 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
   //       slot of R' (its staging reads have completed)                               | Ba |
   //   P2  stage 2 of tile m in R                                                       | Bb |
   int64_t m = wg_in_grp;
+  STAMP(0);
   for (int it = 0; m < n_mtiles || it > 0; ++it, m += gstride) {
     char* region = lds + (it & 1) * REGION;
     char* other = lds + ((it + 1) & 1) * REGION;
     const int par = it & 1;
     const bool have = m < n_mtiles;
+    const int sb = 1 + 6 * (it < 9 ? it : 9);       // stamp slots: iterations 0-8, then the latest
+    STAMP(sb);
     if (have) {
       wait_vmcnt<0>();                              // this wave's x (and its older y stores)
+      STAMP(sb + 1);
       stage1(region, par);
     }
+    STAMP(sb + 2);
     if (it > 0) stage3(other, par ^ 1, m - gstride);
     if (m + gstride < n_mtiles) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
       dma_token(m + gstride, other);
     }
+    STAMP(sb + 3);
     if (!have) break;
     lds_barrier();                                  // Ba: X units and scales complete
+    STAMP(sb + 4);
     stage2(region, par);
     lds_barrier();                                  // Bb: Y units complete
+    STAMP(sb + 5);
   }
+  STAMP(63);
 }
 
 }  // namespace bcfft
@@ -485,3 +498,13 @@ void launch_forward_dm8(const void* x, int64_t n, int n_out, const void* spec, c
   else launch_dm8<false>(x, n, n_out, spec, bias, bias_dt, y, s);
 }
 }  // namespace bcfft
+
+#ifdef BCFFT_STAMPS
+// analysis build only: stamp buffer of bc_forward_dm8_kernel (this TU's copy). Slots per wave: 0
+// start | per iteration it < 9 (base 1 + 6 it, then the latest): +0 top, +1 own x landed, +2
+// stage 1 done, +3 stage 3 + DMA issued, +4 after Ba, +5 stage 2 + Bb done | 63 end
+extern "C" int bcfft_set_stamps_dm8(void* buf) {
+  unsigned long long* p = (unsigned long long*)buf;
+  return hipMemcpyToSymbol(HIP_SYMBOL(bcfft::g_stamps), &p, sizeof(p)) == hipSuccess ? 0 : BCFFT_ERR_HIP;
+}
+#endif

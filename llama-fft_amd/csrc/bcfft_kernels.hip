@@ -770,6 +770,9 @@ static int resolve_algo(int algo, int n_in, int block_size, int xdt = -2, bool y
 #ifndef BCFFT_NO_DM256
   if (bcfft::dm256_eligible(n_in, block_size, xdt, yf32)) return BCFFT_ALGO_DFT;
 #endif
+  // K > 4096 at b = 64 (bf16): the streamed-weight DFT kernel once its 16-token tiles fill a few
+  // CUs (N = 64: 36.9 us vs the split-K MFMA kernel's 31.4; N = 1024: 39.5 vs 71.9)
+  if (bcfft::dm64k_eligible(n_in, block_size, xdt, yf32) && n_tokens >= BCFFT_DM64K_MIN_TOKENS) return BCFFT_ALGO_DFT;
   // K > 4096 at b = 128 (bf16): the streamed-weight DFT kernel, from one token up (it beats the
   // split-K MFMA kernel at every measured N: 20.9 vs 23.4 us at N = 1, profiles/r02_dmk_decode_sizes.log)
   if (bcfft::dmk_eligible(n_in, block_size, xdt, yf32) && n_tokens >= BCFFT_DMK_MIN_TOKENS) return BCFFT_ALGO_DFT;
@@ -833,7 +836,8 @@ int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_featur
     return refuse("bcfft_forward", algo, n_in, block_size, x_dtype, y_dtype);
   const bool dmk = bcfft::dmk_eligible(n_in, block_size, x_dtype, y_dtype == BCFFT_F32);
   const bool dm256 = bcfft::dm256_eligible(n_in, block_size, x_dtype, y_dtype == BCFFT_F32);
-  if (algo == BCFFT_ALGO_DFT && !bcfft::dm_eligible(n_in, block_size) && !dm64 && !dmk && !dm256)
+  const bool dm64k = bcfft::dm64k_eligible(n_in, block_size, x_dtype, y_dtype == BCFFT_F32);
+  if (algo == BCFFT_ALGO_DFT && !bcfft::dm_eligible(n_in, block_size) && !dm64 && !dmk && !dm256 && !dm64k)
     return refuse("bcfft_forward", algo, n_in, block_size, x_dtype, y_dtype);
   algo = resolve_algo(algo, n_in, block_size, x_dtype, y_dtype == BCFFT_F32, n_tokens);
   // the workspace is used only when it is as large as bcfft_forward_workspace_bytes_io asks
@@ -847,6 +851,10 @@ int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_featur
   }
   if (algo == BCFFT_ALGO_DFT && dm256) {
     bcfft::launch_forward_dm256(x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, s);
+    return record_launch();
+  }
+  if (algo == BCFFT_ALGO_DFT && dm64k) {
+    bcfft::launch_forward_dm64k(x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, s);
     return record_launch();
   }
   if (algo == BCFFT_ALGO_DFT && block_size == 64) {

@@ -1122,7 +1122,7 @@ void launch_stat_image(int b, int n_out, int n_in, void* spec, hipStream_t s) {
     launch_dmk_image(n_out, n_in, spec, s);
     return;
   }
-  if (!stat_eligible(n_in, b) && !dm256_geometry(n_in, b)) return;
+  if (!stat_eligible(n_in, b) && !dm256_geometry(n_in, b) && !dm64k_geometry(n_in, b)) return;
   const SpecLayout sl = spec_layout(n_out, n_in, b);
   const int64_t total = (int64_t)sl.stat_groups * 8 * sl.stat_pieces * 64;
   const unsigned blocks = (unsigned)((total + 255) / 256 < 65535 ? (total + 255) / 256 : 65535);

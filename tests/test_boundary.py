@@ -54,12 +54,12 @@ def test_status_strings_and_sizes(built_lib):
             img = -(-ni // 8) * (b // 2) * 2 * (-(-no // opw) * opw) * 8 * 4
         # (+ the per-output-block inverse weight scales: 32 fp32 per group)
         stat = 0
-        if (b == 128 and ni == 32) or (b == 64 and ni in (32, 64)) or (b == 256 and 1 <= ni <= 127):
+        if (b == 128 and ni == 32) or (b == 64 and (ni in (32, 64) or 64 < ni <= 255)) or (b == 256 and 1 <= ni <= 127):
             stat = 16 + -(-no // 32) * 8 * ((b // 16) * -(-ni // 16) * 2) * 64 * 16 + -(-no // 32) * 32 * 4
         elif b == 128 and 32 < ni <= 127:
             stat = 16 + -(-no // 32) * -(-ni // 16) * 128 * 64 * 16 + -(-no // 32) * 32 * 4
         return (no * ni * (b // 2) + b) * 8 + img + stat
-    for no, ni, b in [(32, 32, 128), (86, 32, 128), (32, 86, 128), (40, 48, 128), (8, 160, 128), (64, 64, 64), (2, 4, 32), (16, 16, 256), (16, 43, 256), (43, 8, 256), (2, 128, 256)]:
+    for no, ni, b in [(32, 32, 128), (86, 32, 128), (32, 86, 128), (40, 48, 128), (8, 160, 128), (64, 64, 64), (2, 4, 32), (16, 16, 256), (16, 43, 256), (43, 8, 256), (2, 128, 256), (64, 172, 64), (3, 256, 64)]:
         assert lib.bcfft_spectra_bytes(no, ni, b) == expect(no, ni, b)
     assert lib.bcfft_spectra_bytes(2, 2, 100) == -1
     assert lib.bcfft_spectra_bytes(0, 2, 64) == -1
