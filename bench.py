@@ -314,12 +314,24 @@ def run_variants(dev, algo, steps):
         vw, vkern = time_layer(vl, vx, max(10, steps // 2), 5)
         os.environ["BCFFT_ALGO"] = algo
         vbytes = algo_bytes(vn, vk, vm, vb, vio, False)
-        variants.append({"workload": f"{vk}->{vm} b={vb} N={vn} {vio}-io algo={va}",
-                         "engine": resolved_kernel(va, vk, vb, vio, vm)[1].replace("bc_forward_", "").replace("_kernel", ""),
-                         "ms": round(vkern, 4),
-                         "GTok_elem_s": round(vn * vm / (vkern * 1e-3) / 1e9, 3),
-                         "GB_s": round(vbytes / (vkern * 1e-3) / 1e9, 1),
-                         "frac": round(vbytes / (vkern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+        entry = {"workload": f"{vk}->{vm} b={vb} N={vn} {vio}-io algo={va}",
+                 "engine": resolved_kernel(va, vk, vb, vio, vm)[1].replace("bc_forward_", "").replace("_kernel", ""),
+                 "ms": round(vkern, 4),
+                 "GTok_elem_s": round(vn * vm / (vkern * 1e-3) / 1e9, 3),
+                 "GB_s": round(vbytes / (vkern * 1e-3) / 1e9, 1),
+                 "frac": round(vbytes / (vkern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        if vn <= 1024:
+            # launch-bound size: the same forward replayed from a HIP graph (bcfft.graph), 10
+            # forwards per graph, so the figure is the GPU's and not the host's per-call cost
+            from bcfft.graph import GraphedCall
+            os.environ["BCFFT_ALGO"] = va
+            g = GraphedCall(lambda t: vl(t), [vx], repeat=10)
+            os.environ["BCFFT_ALGO"] = algo
+            gk = time_fn(g.replay, max(10, steps // 2), 3, None, dev)[1] / 10
+            entry["graph_ms"] = round(gk, 4)
+            entry["graph_GB_s"] = round(vbytes / (gk * 1e-3) / 1e9, 1)
+            del g
+        variants.append(entry)
         del vl, vx
     variants.append(time_glu(dev, max(10, steps // 2)))
     return variants
