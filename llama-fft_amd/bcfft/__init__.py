@@ -1,5 +1,5 @@
 """bcfft — MI355X-native block-circulant linear engine (Python side of libbcfft.so)."""
-from . import _lib, graph, ops  # noqa: F401
+from . import _lib, graph, ops, torch_ops  # noqa: F401
 from ._lib import LIB_PATH, SUPPORTED_BLOCKS, load  # noqa: F401
 
-__all__ = ["ops", "graph", "load", "LIB_PATH", "SUPPORTED_BLOCKS"]
+__all__ = ["ops", "graph", "torch_ops", "load", "LIB_PATH", "SUPPORTED_BLOCKS"]

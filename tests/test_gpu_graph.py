@@ -35,3 +35,19 @@ def test_graph_replay_matches_eager(dev, k, m, b, io, n):
     assert torch.equal(y2, fwd(x2))
     with pytest.raises(ValueError):
         g(torch.randn(n + 1, k, device=dev).to(io))
+
+
+def test_torch_library_ops_match_bcfft_ops(dev):
+    """torch.ops.bcfft.* run the same kernels as bcfft.ops (bit-identical), and torch.library's
+    opcheck accepts the registrations (schema, fake kernel vs the real one)."""
+    import bcfft.torch_ops  # noqa: F401
+    from bcfft import ops
+    torch.manual_seed(1)
+    c = torch.randn(32, 32, 128, device=dev) * 0.01
+    x = torch.randn(64, 4096, device=dev).to(torch.bfloat16)
+    spec = torch.ops.bcfft.spectra(c, False)
+    assert torch.equal(spec, ops.spectra(c))
+    y = torch.ops.bcfft.forward(x, spec, None, 128, 4096, "auto")
+    assert torch.equal(y, ops.forward(x, spec, None, 128, 4096, algo="auto"))
+    torch.library.opcheck(torch.ops.bcfft.forward.default, (x, spec, None, 128, 4096, "auto"),
+                          test_utils=("test_schema", "test_faketensor"))
