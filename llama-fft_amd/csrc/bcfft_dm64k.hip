@@ -45,6 +45,13 @@ constexpr int LDS_BYTES = OS_OFF + 128;
 constexpr int FRAGS = BW * KC * NT;                 // B fragments per wave and chunk
 constexpr int NDMA = 2 * 4;                         // 1-KiB x DMA pieces per wave and chunk (2 tokens)
 constexpr int HEAD = 4;
+// analysis builds only (results are WRONG when set): 1 no B loads, 2 no stage-1 arithmetic, 4 no
+// stage-2 MFMAs, 8 no stage 3, 16 no x DMA, 32 no y stores
+#ifdef BCFFT_DM64K_ABL
+constexpr int ABL = BCFFT_DM64K_ABL;
+#else
+constexpr int ABL = 0;
+#endif
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 static_assert(XSLOT % 256 == 64, "slot stride 64 B off the bank period");
 
@@ -84,6 +91,17 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
   // 8q + (lane >> 3) of 128 B, unit u of row r at u ^ (r & 7); the buffer range ends at the row
   // end, so a partial last chunk and tokens / tiles past the end land as zeros
   auto dma_chunk = [&](int64_t m, int c, char* region) {
+    if constexpr ((ABL & 16) != 0) {                // keep the VMEM count: 8 empty-range loads
+      const __amdgpu_buffer_rsrc_t zr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(xv), 0, 0, 0x00020000);
+      const uint32_t d0 = lds_base + (uint32_t)(region - lds) + wave * XSLOT;
+#pragma unroll
+      for (int q = 0; q < NDMA; ++q) {
+        uint32_t keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(0), "s"(zr), "s"(d0) : "memory");
+      }
+      return;
+    }
     const int dl = opaque(lane);
     const int r = dl >> 3;
     const int vb = r * 128 + 16 * ((dl & 7) ^ r);
@@ -114,7 +132,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
   // fragment (fb, j, nt) of chunk c; K-step 2c + 1 past the image (odd KS, last chunk) reads zeros
   auto load_b1 = [&](int c, int fb, int j, int nt, u32x4 (&breg)[BW][KC][NT]) {
     const int ks = 2 * c + j;
-    const int vo = opaque(lane) * 16 + (ks < KS ? (fb * KS + ks) * 2 + nt : npiece) * 1024;
+    const int vo = opaque(lane) * 16 + (ks < KS && (ABL & 1) == 0 ? (fb * KS + ks) * 2 + nt : npiece) * 1024;
     asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(breg[fb][j][nt]) : "v"(vo), "s"(brs));
   };
   auto wait_b = [&](auto n_tag, u32x4 (&breg)[BW][KC][NT]) {
@@ -143,6 +161,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
   // ---- stage 1 (wave w: tokens w, w + 8): bcfft_dm64.hip's stage 1 on the chunk's two quarters,
   // the scale of each lowered by HEAD bits
   auto stage1 = [&](char* region) {
+    if constexpr ((ABL & 2) != 0) {
+      if (lane < 2) { wsc[wave * 2 + lane] = 0; wsc[(wave + 8) * 2 + lane] = 0; }
+      return;
+    }
     const int l = opaque(lane);
     const int b16 = l & 15, g = l >> 4;
     const int q4 = (l & 15) >> 2, p4 = l & 3;
@@ -317,8 +339,11 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
           const f16x8 a = __builtin_bit_cast(f16x8, raw);
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt)
-            acc[fb][mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, __builtin_bit_cast(f16x8, breg[fb][j][nt]),
-                                                                     acc[fb][mt][nt], 0, 0, 0);
+            if constexpr ((ABL & 4) != 0)
+              acc[fb][mt][nt] += f32x4{a[0], a[1], __builtin_bit_cast(f16x8, breg[fb][j][nt])[0], 0.f};
+            else
+              acc[fb][mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, __builtin_bit_cast(f16x8, breg[fb][j][nt]),
+                                                                       acc[fb][mt][nt], 0, 0, 0);
         }
         if (nb >= 0) {
           load_b1(nc, fb, j, 0, breg);
@@ -374,6 +399,12 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
   // ---- stage 3 (token slot tl of a region, reference exponent rref): bcfft_dm64.hip's stage 3;
   // tok < 0 stores nothing (the stores are still issued, with an empty range)
   auto stage3 = [&](char* region, int tl, int rref, int64_t tok) {
+    if constexpr ((ABL & 8) != 0) {                 // keep the VMEM count: 4 empty-range stores
+      const __amdgpu_buffer_rsrc_t zr = __builtin_amdgcn_make_buffer_rsrc(yv, 0, 0, 0x00020000);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, zr, 0, 0, 0);
+      return;
+    }
     const int l = opaque(lane);
     const int o16 = l & 15, g = l >> 4;
     char* slot = region + tl * XSLOT;
@@ -399,7 +430,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
         gt[mt][pr] = *reinterpret_cast<const f16x8*>(lds + F_OFF + 128 * t + 16 * ((4 * pr + g) ^ fsw64(t)));
       }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // Y is in registers: the slot is free
-    const bool tok_ok = tok >= 0 && tok < n_tokens;
+    const bool tok_ok = tok >= 0 && tok < n_tokens && (ABL & 32) == 0;
     const int nvalid = n_out - grp_o * NOG;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {

@@ -1,0 +1,15 @@
+#!/bin/bash
+# A/B timing of experiment builds on the b = 64 rows in one GPU session.
+# usage: tools/ab_b64.sh TAG lib1 lib2 ...   (lib names under llama-fft_amd/lib/, "" = product)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+TAG=$1; shift
+for round in 1 2; do
+  for L in "$@"; do
+    P=$PWD/llama-fft_amd/lib/${L:-libbcfft.so}
+    echo "== $L round $round" >> gpurun_out/ab_$TAG.log
+    BCFFT_LIB_PATH=$P timeout -k 10 120 python3 tools/time_algos.py dft --b64down >> gpurun_out/ab_$TAG.log 2>&1 || exit 1
+  done
+done
+grep -v amdgpu gpurun_out/ab_$TAG.log
