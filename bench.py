@@ -64,6 +64,10 @@ def resolved_kernel(algo, k, b, io="fp32", m=4096):
         return ("dft", "bc_forward_dm64k_kernel",
                 "MFMA fp16 throughout, b=64, 16 tokens per tile, 32-block K-chunks with weight fragments "
                 "streamed from L2 (bf16 I/O)")
+    if io == "bf16" and algo in ("dft", "auto") and b == 64 and n_in == 64 and m > 64 * b:
+        return ("dft", "bc_forward_dm64g_kernel",
+                "MFMA fp16 throughout, b=64, 8 tokens per tile, stage 1 once per tile, every output group's "
+                "weight fragments streamed from L2 (bf16 I/O)")
     if io == "bf16" and algo in ("dft", "auto") and b == 64 and n_in == 64:
         return ("dft", "bc_forward_dm64_kernel",
                 "MFMA fp16 throughout, b=64, 8 tokens per tile, one-term spectra (bf16 I/O)")

@@ -574,6 +574,11 @@ void launch_forward_dmg(const void* x, int64_t n, int n_out, const void* spec, c
 bool dm64_eligible(int n_in, int b, int xdt, bool yf32);
 void launch_forward_dm64(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt,
                          void* y, bool glu, hipStream_t s);
+// several output groups at b = 64 (bcfft_dm64g.hip): stage 1 once per tile, the groups' weight
+// fragments streamed from L2
+bool dm64g_eligible(int n_in, int b, int xdt, bool yf32, int n_out, bool glu);
+void launch_forward_dm64g(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt,
+                          void* y, bool glu, hipStream_t s);
 void launch_forward_dm8(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt, void* y,
                         bool glu, hipStream_t s);
 // b = 256, n_in <= 127, bf16 x and bf16 y (no bias or a bf16 bias) (bcfft_dm256.hip)

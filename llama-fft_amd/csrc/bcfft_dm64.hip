@@ -426,6 +426,12 @@ bool dm64_eligible(int n_in, int b, int xdt, bool yf32) { return b == 64 && n_in
 
 void launch_forward_dm64(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt,
                          void* y, bool glu, hipStream_t s) {
+#ifndef BCFFT_NO_DM64G
+  if (dm64g_eligible(64, 64, BCFFT_BF16, false, n_out, glu)) {   // several groups: x transformed once
+    launch_forward_dm64g(x, n, n_out, spec, bias, bias_dt, y, glu, s);
+    return;
+  }
+#endif
   if (glu) launch_dm64<true>(x, n, n_out, spec, nullptr, BCFFT_NONE, y, s);
   else launch_dm64<false>(x, n, n_out, spec, bias, bias_dt, y, s);
 }

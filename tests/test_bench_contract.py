@@ -27,7 +27,8 @@ def test_engine_resolution_mirrors_auto_rule():
     assert bench.resolved_kernel("auto", 11008, 128)[1] == "bc_forward_mfma_kernel"
     assert bench.resolved_kernel("auto", 4096, 256)[1] == "bc_forward_valu_kernel"
     assert bench.resolved_kernel("auto", 4096, 128, "bf16")[1] == "bc_forward_dm8_kernel"
-    assert bench.resolved_kernel("auto", 4096, 64, "bf16")[1] == "bc_forward_dm64_kernel"
+    assert bench.resolved_kernel("auto", 4096, 64, "bf16")[1] == "bc_forward_dm64_kernel"    # 2 output groups
+    assert bench.resolved_kernel("auto", 4096, 64, "bf16", 11008)[1] == "bc_forward_dm64g_kernel"
     assert bench.resolved_kernel("auto", 2048, 64, "bf16")[1] == "bc_forward_stat_kernel"
     assert bench.resolved_kernel("valu", 4096, 128)[1] == "bc_forward_valu_kernel"
 

@@ -81,6 +81,9 @@ if __name__ == "__main__":
     if "--b64" in sys.argv:                         # the b = 64 sweep rows (bcfft_dm64.hip, bcfft_dm64k.hip)
         shapes = [(4096, 4096, 64, "bf16", 8192), (4096, 11008, 64, "bf16", 8192), (11008, 4096, 64, "bf16", 8192),
                   (11008, 4096, 64, "bf16", 1024), (11008, 4096, 64, "bf16", 64)]
+    if "--b64up" in sys.argv:                       # b = 64, K = 4096: 2 and 6 output groups, fused gate/up
+        shapes = [(4096, 4096, 64, "bf16", 8192), (4096, 11008, 64, "bf16", 8192), (4096, 11008, 64, "bf16", 1700)]
+        t_glu(b=64)
     if "--b256" in sys.argv:                        # the b = 256 sweep rows (bcfft_dm256.hip)
         shapes = [(4096, 4096, 256, "bf16", 8192), (4096, 11008, 256, "bf16", 8192), (11008, 4096, 256, "bf16", 8192),
                   (11008, 4096, 256, "bf16", 1024), (11008, 4096, 256, "bf16", 64)]
