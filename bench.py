@@ -71,6 +71,10 @@ def resolved_kernel(algo, k, b, io="fp32", m=4096):
     if io == "bf16" and algo in ("dft", "auto") and b == 64 and n_in == 64:
         return ("dft", "bc_forward_dm64_kernel",
                 "MFMA fp16 throughout, b=64, 8 tokens per tile, one-term spectra (bf16 I/O)")
+    if io == "bf16" and algo in ("dft", "auto") and b == 256 and n_in == 16 and m > 32 * b:
+        return ("dft", "bc_forward_dm256g_kernel",
+                "MFMA fp16 throughout, b=256 as three 128-point virtual rows, stage 1 once per 8-token tile, "
+                "every output group's weight fragments streamed from L2 (bf16 I/O)")
     if io == "bf16" and algo in ("dft", "auto") and b == 256 and n_in == 16:
         return ("dft", "bc_forward_dm256_kernel",
                 "MFMA fp16 throughout, b=256 as three 128-point virtual rows, 8 tokens per tile, "

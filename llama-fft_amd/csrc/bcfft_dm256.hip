@@ -995,6 +995,448 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256k_kernel(
 
 // ---- weight image at b = 256: the generic STAT image kernels instantiated for B = 256 (groups
 // of 32 output blocks = two N-tiles; a b = 256 workgroup takes one N-tile)
+
+// ============================================================== several output groups
+// bc_forward_dm256g_kernel: b = 256, K = 4096, M > 4096 (three or more groups of 16 output
+// blocks: the sweep's 4096 -> 11008). bcfft_dmg.hip's scheme on the b = 256 stages: stage 1 once
+// per 8-token tile (bc_forward_dm256_kernel's), the A fragments of the wave's 16 bins for all 8
+// tokens into VGPRs (64), then per output group: stage 2 against the group's 16 B fragments per
+// wave, streamed from L2 in two passes of 8 (double-buffered, compiler-visible loads), Y units
+// into the tile's slots, stage 3 of token w with the group's 16 rows stored. Numerics are
+// bc_forward_dm256_kernel's in the same order: bit-identical to it run per group.
+namespace d256 {
+constexpr int MAXG = 64;
+constexpr int OSG_OFF = SC_OFF + 128;               // inverse weight scales [MAXG][16]
+constexpr int LDSG_BYTES = OSG_OFF + MAXG * NOB * 4;
+static_assert(LDSG_BYTES <= 160 * 1024, "LDS budget");
+}  // namespace d256
+
+__global__ __launch_bounds__(512, 2) void bc_forward_dm256g_kernel(
+    const void* __restrict__ xv, int64_t n_tokens, int n_out, const uint32_t* __restrict__ stat,
+    const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
+  using namespace d256;
+  constexpr int XT = BCFFT_BF16;
+  constexpr int ES = 2, ESY = 2;
+  constexpr int PF = 8;                             // fragments per stage-2 pass
+
+  __shared__ __attribute__((aligned(16))) char lds[LDSG_BYTES];
+  int* wsc = reinterpret_cast<int*>(lds + SC_OFF);
+  const float2* cs_l = reinterpret_cast<const float2*>(lds + CS_OFF);
+  const float* osl = reinterpret_cast<const float*>(lds + OSG_OFF);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n_groups = (n_out + NOB - 1) / NOB;
+  const int64_t M = (int64_t)n_out * B;
+  const int64_t n_mtiles = (n_tokens + TT - 1) / TT;
+  const int64_t gstride = gridDim.x;
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+  const uint4* bimg = reinterpret_cast<const uint4*>(stat + 4);
+
+  auto dma_token = [&](int64_t m, char* region) {
+    const int64_t tok = m * TT + wave;
+    const bool ok = tok < n_tokens;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>((const char*)xv) + (ok ? tok : 0) * K * ES, 0, ok ? K * ES : 0, 0x00020000);
+    const int dl = opaque(lane);
+    const uint32_t dst0 = lds_base + (uint32_t)(region - lds) + wave * SLOT;
+    int vb[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int h = dl >> 5;
+      vb[c] = h * 512 + 16 * ((dl & 31) ^ ((2 * c + h) & 15));
+    }
+#pragma unroll
+    for (int q = 0; q < NDMA; ++q) {
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(vb[q & 7]), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
+    }
+  };
+
+  // ---- B fragments of output group g (STAT image group g >> 1, N-tile g & 1), pass p: bins
+  // 8p .. 8p + 7 of the wave (piece (fb * 1 + 0) * 2 + nt)
+  typedef u32x4 Breg[PF];
+  auto b_rsrc = [&](int g) {
+    return __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint4*>(bimg + ((int64_t)((g >> 1) * NW + wave) * NPIECE) * 64), 0, NPIECE * 1024, 0x00020000);
+  };
+  auto load_pass = [&](int g, int p, Breg& br) {
+    const __amdgpu_buffer_rsrc_t brs = b_rsrc(g);
+    const int vo = opaque(lane) * 16;
+#pragma unroll
+    for (int j = 0; j < PF; ++j)
+      br[j] = __builtin_amdgcn_raw_buffer_load_b128(brs, vo, ((8 * p + j) * 2 + (g & 1)) * 1024, 0);
+  };
+
+  // ---- prologue: the first tile's x, the tables, every group's inverse weight scales, the first
+  // group's first B pass
+  Breg breg[2];
+  const int64_t m0 = blockIdx.x;
+  if (m0 < n_mtiles) dma_token(m0, lds);
+  {
+    const uint4* tab = reinterpret_cast<const uint4*>(kDmF);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int c = tid + 512 * r;
+      const int t = c >> 4, ch = c & 15;
+      *reinterpret_cast<uint4*>(lds + F_OFF + 256 * t + 16 * (ch ^ fsw(t))) = tab[c];
+    }
+    if (tid < 128) {
+      double sn, cn;
+      sincospi((double)tid / 128.0, &sn, &cn);
+      reinterpret_cast<float2*>(lds + CS_OFF)[tid] = make_float2((float)cn, (float)sn);
+    }
+    for (int e = tid; e < n_groups * NOB; e += 512) reinterpret_cast<float*>(lds + OSG_OFF)[e] = osc[e];
+  }
+  wait_vmcnt<0>();
+  load_pass(0, 0, breg[0]);
+  lds_barrier();
+
+  auto stage1 = [&](char* region, int par) {
+    const int l = opaque(lane);
+    const int b16 = l & 15, g = l >> 4;
+    char* slot = region + wave * SLOT;
+    const int q4 = (l & 15) >> 2, p4 = l & 3;
+    const int cx = (p4 >> 1) ^ fsw(8 * g + q4);
+    const int trb = F_OFF + 256 * (8 * g + q4) + 8 * (p4 & 1);
+    const char* rowp = slot + b16 * (B * ES);
+    // x[4 quarter + ...]: unit (8 qt + 4 ks + g) of the row, 8 bf16 each
+    uint32_t xr[4][2][4];
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const uint4 w = *reinterpret_cast<const uint4*>(rowp + 16 * ((8 * qt + 4 * ks + g) ^ b16));
+        xr[qt][ks][0] = w.x; xr[qt][ks][1] = w.y; xr[qt][ks][2] = w.z; xr[qt][ks][3] = w.w;
+      }
+    float m0f = 0.f, m1f = 0.f;                     // max |x| over the token
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const float2 f0 = unpack16<XT>(xr[qt][ks][e]), f1 = unpack16<XT>(xr[qt][ks][e + 1]);
+          m0f = amax3(m0f, f0.x, f0.y);
+          m1f = amax3(m1f, f1.x, f1.y);
+        }
+    const float mxf = __builtin_fmaxf(m0f, m1f);
+    // |a + a'|, |p +- p'|, |q +- q'| <= 4 max |x|
+    const int sx = stat_scale_exp(4.f * __uint_as_float(wave_umax(__float_as_uint(mxf))));
+    if (l < 2) wsc[par * 16 + wave * 2 + l] = sx - 7;   // X = D 2^-(sx - 7): the table's 2^-7
+    const float S = __int_as_float((sx + 127) << 23);
+    // B fragments (8 t each) of the six transform inputs per K-step
+    uint32_t fa[2][2][4], fp[2][2][4], fq[2][2][4];   // [ks][prime / double prime][e]
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const float4* csp = reinterpret_cast<const float4*>(cs_l + 32 * ks + 8 * g);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float4 cs2 = csp[e];                   // (cos, sin) of t = 32 ks + 8 g + 2 e, + 1
+        const float2 x0 = unpack16<XT>(xr[0][ks][e]), x1 = unpack16<XT>(xr[1][ks][e]);
+        const float2 x2 = unpack16<XT>(xr[2][ks][e]), x3 = unpack16<XT>(xr[3][ks][e]);
+        float ap[2], app[2], pp[2], ppp[2], qp[2], qpp[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float xt = h ? x0.y : x0.x, xt64 = h ? x1.y : x1.x, xt128 = h ? x2.y : x2.x, xt192 = h ? x3.y : x3.x;
+          const float c = h ? cs2.z : cs2.x, s = h ? cs2.w : cs2.y;
+          const float u = (xt + xt128) * S, v = (xt64 + xt192) * S;
+          const float d0 = (xt - xt128) * S, d1 = (xt64 - xt192) * S;
+          ap[h] = u + v;
+          app[h] = u - v;
+          pp[h] = fmaf(d0, c, -d1 * s);             // p_t + p_{t+64}
+          ppp[h] = fmaf(d0, c, d1 * s);             // p_t - p_{t+64}
+          qp[h] = -fmaf(d0, s, d1 * c);             // q_t + q_{t+64}
+          qpp[h] = fmaf(d1, c, -d0 * s);            // q_t - q_{t+64}
+        }
+        fa[ks][0][e] = pk_rne(ap[0], ap[1]);
+        fa[ks][1][e] = pk_rne(app[0], app[1]);
+        fp[ks][0][e] = pk_rne(pp[0], pp[1]);
+        fp[ks][1][e] = pk_rne(ppp[0], ppp[1]);
+        fq[ks][0][e] = pk_rne(qp[0], qp[1]);
+        fq[ks][1][e] = pk_rne(qpp[0], qpp[1]);
+      }
+    }
+    // X write lane bases: D^T row 4 g + r of tile (pr, mt) is b = 128 packed bin
+    // f = 16 mt + 4 g + pr (+ 2 for r >= 2): b = 256 bin 2 f (a) or 2 f + 1 (p, q)
+    // pass 1: the a rows -> even bins
+    {
+      f32x4 acc[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) {
+            const int cb = 16 * ((8 * pr + 2 * mt) ^ cx);
+            const char* p0 = lds + trb + 256 * 32 * ks + cb;
+            const s16x4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p0));
+            const s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p0 + 256 * 4));
+            const f16x8 af = __builtin_bit_cast(f16x8, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+            acc[4 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                af, frag(fa[ks][pr][0], fa[ks][pr][1], fa[ks][pr][2], fa[ks][pr][3]), acc[4 * pr + mt], 0, 0, 0);
+          }
+      // stage-1 outputs of pass 2 (p, q) come from the same registers-only inputs, so the even
+      // X units may overwrite the x rows now: every x read of this wave is done (in-order DS)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const int f = 16 * mt + 4 * g + pr;
+          *reinterpret_cast<uint32_t*>(slot + xunit(2 * f, 0) + 4 * b16) = pk_rne(acc[4 * pr + mt][0], acc[4 * pr + mt][1]);
+          *reinterpret_cast<uint32_t*>(slot + xunit(2 * f + 4, 0) + 4 * b16) = pk_rne(acc[4 * pr + mt][2], acc[4 * pr + mt][3]);
+        }
+    }
+    // pass 2: the p and q rows -> odd bins X_{2f+1} = P_f + i Q_f (bin 1: (P_0, Q_0))
+    {
+      f32x4 accp[8], accq[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        accp[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        accq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) {
+            const int cb = 16 * ((8 * pr + 2 * mt) ^ cx);
+            const char* p0 = lds + trb + 256 * 32 * ks + cb;
+            const s16x4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p0));
+            const s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p0 + 256 * 4));
+            const f16x8 af = __builtin_bit_cast(f16x8, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+            accp[4 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                af, frag(fp[ks][pr][0], fp[ks][pr][1], fp[ks][pr][2], fp[ks][pr][3]), accp[4 * pr + mt], 0, 0, 0);
+            accq[4 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                af, frag(fq[ks][pr][0], fq[ks][pr][1], fq[ks][pr][2], fq[ks][pr][3]), accq[4 * pr + mt], 0, 0, 0);
+          }
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const f32x4 P = accp[4 * pr + mt], Q = accq[4 * pr + mt];
+          const int f = 16 * mt + 4 * g + pr;
+          float re0 = P[0] - Q[1], im0 = P[1] + Q[0];
+          if (mt == 0 && pr == 0 && g == 0) {       // packed bin 0 = (P_0, P_64): X_1 = P_0 + i Q_0
+            re0 = P[0];
+            im0 = Q[0];
+          }
+          *reinterpret_cast<uint32_t*>(slot + xunit(2 * f + 1, 0) + 4 * b16) = pk_rne(re0, im0);
+          *reinterpret_cast<uint32_t*>(slot + xunit(2 * f + 5, 0) + 4 * b16) = pk_rne(P[2] - Q[3], P[3] + Q[2]);
+        }
+    }
+  };
+
+  // ---- A fragments of the wave's bins k = 16 wave + fb for all 8 tokens, once per tile
+  // (bc_forward_dm256_kernel's stage-2 operand: re rows [Xr, Xi], im rows [Xi, -Xr]; bin 0 with
+  // the extra 1/2; one scale per token, so no alignment)
+  f16x8 areg[BPW];
+  auto load_a = [&](char* region) {
+    const int ml = opaque(lane);
+    const int arow = ml & 15, kb = ml >> 4;
+    const int a_t = arow >> 1, a_reim = arow & 1;
+    const uint32_t a_sel = a_reim ? 0x01000302u : 0x03020100u;
+    const uint32_t hh = 15u << 10, h0 = 14u << 10;
+    const uint32_t amul = a_reim ? (hh | ((hh | 0x8000u) << 16)) : (hh | (hh << 16));
+    const uint32_t amul0 = a_reim ? (h0 << 16) : h0;
+    const char* ab = region + a_t * SLOT + 16 * kb;
+#pragma unroll
+    for (int fb = 0; fb < BPW; ++fb) {
+      const int k = wave * BPW + fb;
+      uint4 raw = *reinterpret_cast<const uint4*>(ab + xunit(k, 0));
+      if (k == 0) {
+        raw.x = pkmul(raw.x, amul0); raw.y = pkmul(raw.y, amul0);
+        raw.z = pkmul(raw.z, amul0); raw.w = pkmul(raw.w, amul0);
+      } else {
+        raw.x = pkmul(__builtin_amdgcn_perm(raw.x, raw.x, a_sel), amul);
+        raw.y = pkmul(__builtin_amdgcn_perm(raw.y, raw.y, a_sel), amul);
+        raw.z = pkmul(__builtin_amdgcn_perm(raw.z, raw.z, a_sel), amul);
+        raw.w = pkmul(__builtin_amdgcn_perm(raw.w, raw.w, a_sel), amul);
+      }
+      areg[fb] = __builtin_bit_cast(f16x8, raw);
+    }
+  };
+
+  // ---- stage 2 of group g: two passes of 8 bins over the double-buffered B registers (both in
+  // flight on entry); Y units (bc_forward_dm256_kernel's map) into the tile's slots
+  auto stage2 = [&](char* region) {
+    constexpr float YS = 1.f / 2097152.f;
+    uint32_t yh[BPW][2];
+#pragma unroll
+    for (int fb = 0; fb < BPW; ++fb) {
+      const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(areg[fb], __builtin_bit_cast(f16x8, breg[fb >> 3][fb & 7]),
+                                                                f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) yh[fb][s2] = pk_rne(acc[2 * s2] * YS, acc[2 * s2 + 1] * YS);
+    }
+    const int ml = opaque(lane);
+    const int yt = ml >> 4;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      char* yb = region + (2 * yt + s2) * SLOT + 16 * (ml & 15);
+      *reinterpret_cast<uint4*>(yb + yunit(0, wave, 0, 0)) = make_uint4(yh[0][s2], yh[4][s2], yh[8][s2], yh[12][s2]);
+      *reinterpret_cast<uint4*>(yb + yunit(0, wave, 0, 1)) = make_uint4(yh[2][s2], yh[6][s2], yh[10][s2], yh[14][s2]);
+      *reinterpret_cast<uint4*>(yb + yunit(1, wave, 0, 0)) = make_uint4(yh[1][s2], yh[5][s2], yh[9][s2], yh[13][s2]);
+      *reinterpret_cast<uint4*>(yb + yunit(1, wave, 0, 1)) = make_uint4(yh[3][s2], yh[7][s2], yh[11][s2], yh[15][s2]);
+    }
+  };
+
+  auto stage3 = [&](char* region, int par, int64_t mp, int grp, auto&& before_stores) {
+    const int l = opaque(lane);
+    const int o16 = l & 15, g = l >> 4;
+    char* slot = region + wave * SLOT;
+    const int nmin = wsc[par * 16 + wave * 2];
+    const float ysc = __builtin_ldexpf(osl[grp * NOB + o16], 30 - nmin);
+    // Y fragments: B[k = 8 g + j][o] of virtual wave 4 ks + g, parity pr, spectrum s
+    uint4 ye[2][2], yz[2][2], yw[2][2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        ye[ks][pr] = *reinterpret_cast<const uint4*>(slot + yunit(0, 4 * ks + g, o16, pr));
+        yz[ks][pr] = *reinterpret_cast<const uint4*>(slot + yunit(1, 4 * ks + g, o16, pr));
+      }
+    const int gx = g ^ fsw(o16);
+    const char* gb = lds + F_OFF + 256 * o16;
+    auto gload = [&](int mt, f16x8 (&gf)[2][2]) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr)
+          gf[ks][pr] = *reinterpret_cast<const f16x8*>(gb + 4096 * mt + 16 * ((8 * pr + 4 * ks) ^ gx));
+    };
+    f16x8 gcur[2][2];
+    gload(0, gcur);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // Y is in registers: the slot is free
+    // W' = -i Z: (re, im) -> (im, -re); W and W' packed bin 0 (virtual bin 0 of wave 0: g == 0,
+    // ks 0, parity 0, first pair) = (Re Z_0, 0) and (Im Z_0, 0)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const uint4 z = yz[ks][pr];
+        yw[ks][pr] = make_uint4(__builtin_amdgcn_perm(z.x, z.x, 0x01000302u) ^ 0x80000000u,
+                                __builtin_amdgcn_perm(z.y, z.y, 0x01000302u) ^ 0x80000000u,
+                                __builtin_amdgcn_perm(z.z, z.z, 0x01000302u) ^ 0x80000000u,
+                                __builtin_amdgcn_perm(z.w, z.w, 0x01000302u) ^ 0x80000000u);
+      }
+    if (g == 0) {
+      yw[0][0].x = yz[0][0].x >> 16;
+      yz[0][0].x &= 0xffffu;
+    }
+    const int64_t tok = mp * TT + wave;
+    const bool tok_ok = tok < n_tokens;
+    const int nvalid = n_out - grp * NOB;
+    // staging: row o16 (512 B = 64 units of 8 B), outputs t..t+3 (t = 16 mt + 4 g + 64 hf) in
+    // unit 4 mt + g + 16 hf, t + 128 in unit 32 + ...; physical unit u ^ 2 o16
+    const int sw = 2 * o16;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      f32x4 E[3], O[3];
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        E[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+        O[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        E[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][0], __builtin_bit_cast(f16x8, ye[ks][0]), E[0], 0, 0, 0);
+        O[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][1], __builtin_bit_cast(f16x8, ye[ks][1]), O[0], 0, 0, 0);
+        E[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][0], __builtin_bit_cast(f16x8, yz[ks][0]), E[1], 0, 0, 0);
+        O[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][1], __builtin_bit_cast(f16x8, yz[ks][1]), O[1], 0, 0, 0);
+        E[2] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][0], __builtin_bit_cast(f16x8, yw[ks][0]), E[2], 0, 0, 0);
+        O[2] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][1], __builtin_bit_cast(f16x8, yw[ks][1]), O[2], 0, 0, 0);
+      }
+      if (mt < 3) gload(mt + 1, gcur);
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const float4 c01 = *reinterpret_cast<const float4*>(cs_l + 16 * mt + 4 * g + 64 * hf);
+        const float4 c23 = *reinterpret_cast<const float4*>(cs_l + 16 * mt + 4 * g + 64 * hf + 2);
+        const float cc[4] = {c01.x, c01.z, c23.x, c23.z}, ss[4] = {c01.y, c01.w, c23.y, c23.w};
+        float lo[4], hi[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = hf ? E[0][r] - O[0][r] : E[0][r] + O[0][r];
+          const float w = hf ? E[1][r] - O[1][r] : E[1][r] + O[1][r];
+          const float wp = hf ? E[2][r] - O[2][r] : E[2][r] + O[2][r];
+          const float o = fmaf(cc[r], w, -ss[r] * wp);
+          lo[r] = (e + o) * ysc;                    // y_t
+          hi[r] = (e - o) * ysc;                    // y_{t+128}
+        }
+        if (bias_dt != BCFFT_NONE) {                // .to(x dtype) :266, + bias :270-271
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            lo[r] = round_to(lo[r], XT);
+            hi[r] = round_to(hi[r], XT);
+          }
+          if (o16 < nvalid) {
+            const int64_t cc0 = (int64_t)(grp * NOB + o16) * B + 16 * mt + 4 * g + 64 * hf;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              lo[r] += load_scalar(bias, cc0 + r, bias_dt);
+              hi[r] += load_scalar(bias, cc0 + 128 + r, bias_dt);
+            }
+          }
+        }
+        const int u = 4 * mt + g + 16 * hf;
+        *reinterpret_cast<uint2*>(slot + 512 * o16 + 8 * (u ^ sw)) = make_uint2(pack16<XT>(lo[0], lo[1]), pack16<XT>(lo[2], lo[3]));
+        *reinterpret_cast<uint2*>(slot + 512 * o16 + 8 * ((u + 32) ^ sw)) = make_uint2(pack16<XT>(hi[0], hi[1]), pack16<XT>(hi[2], hi[3]));
+      }
+    }
+    before_stores();
+    // staged rows -> global: each instruction stores 1 KiB = 2 whole rows (32 lanes per row):
+    // 16-B unit w of row r at physical 16-B unit w ^ r (the 8-B swizzle by 2 r keeps pairs)
+    constexpr int RB = B * ESY;
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (char*)yv + (tok_ok ? tok : 0) * M * ESY + (int64_t)grp * NOB * RB, 0,
+        tok_ok ? (int)((M - (int64_t)grp * NOB * B) * ESY) : 0, 0x00020000);
+    const int w = l & 31, lr = l >> 5;
+    uint4 d[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int row = 2 * q + lr;
+      d[q] = *reinterpret_cast<const uint4*>(slot + 512 * row + 16 * (w ^ row));
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs, (2 * q + lr) * RB + 16 * w, 0, 0);
+  };
+
+  // Pipeline per 8-token tile m (bcfft_dmg.hip's; region R = it & 1 holds its x, R' is free):
+  //   LDS-DMA of x(m + stride) into R'; stage 1 of token w in R                       | Ba |
+  //   A fragments -> VGPRs; B pass 1 of group 0                                        | Bx |
+  //   per group g: stage 2 (Y units into R)                                            | Bb |
+  //                B pass 0 of the next group (or of the next tile's group 0); stage 3
+  //                of token w, B pass 1 of the next group, stores                      | Bc |
+  int it = 0;
+  for (int64_t m = m0; m < n_mtiles; m += gstride, ++it) {
+    char* region = lds + (it & 1) * REGION;
+    char* other = lds + ((it + 1) & 1) * REGION;
+    const int par = it & 1;
+    const bool dma = m + gstride < n_mtiles;
+    if (dma) dma_token(m + gstride, other);
+    stage1(region, par);
+    lds_barrier();                                  // Ba: X units and scales complete
+    load_a(region);
+    load_pass(0, 1, breg[1]);
+    lds_barrier();                                  // Bx: every wave holds its A fragments
+    for (int g = 0; g < n_groups; ++g) {
+      stage2(region);
+      lds_barrier();                                // Bb: Y units complete
+      const bool more = g + 1 < n_groups;
+      if (more) load_pass(g + 1, 0, breg[0]);
+      else if (dma) load_pass(0, 0, breg[0]);
+      stage3(region, par, m, g, [&] {
+        if (more) load_pass(g + 1, 1, breg[1]);
+      });
+      lds_barrier();                                // Bc: staging reads done (slots reusable)
+    }
+  }
+}
 }  // namespace bcfft
 
 namespace bcfft {
@@ -1010,6 +1452,14 @@ void launch_forward_dm256(const void* x, int64_t n, int n_in, int n_out, const v
   const int64_t total = group_grid(device_cu_count(), groups, n_mtiles);
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
   const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
+#ifndef BCFFT_NO_DM256G
+  if (n_in == d256::NI && groups >= 3 && groups <= d256::MAXG) {   // several groups: x transformed once
+    const int64_t wgs = device_cu_count() < n_mtiles ? device_cu_count() : n_mtiles;
+    hipLaunchKernelGGL(bc_forward_dm256g_kernel, dim3((unsigned)wgs), dim3(512), 0, s, x, n, n_out, stat, osc, bias,
+                       bias_dt, y);
+    return;
+  }
+#endif
   if (n_in == d256::NI)
     hipLaunchKernelGGL(bc_forward_dm256_kernel, dim3((unsigned)total), dim3(512), 0, s, x, n, n_out, stat, osc, bias,
                        bias_dt, y);

@@ -127,3 +127,19 @@ def test_dm256_full_size_sweep_shape(dev):
     bad = np.abs(g - ref) > 2 * ulp * np.abs(ref) + 2 * ulp * rms
     assert not bad.any(), f"{int(bad.sum())} elements beyond ~1 ulp"
     assert rel_err(g, ref) < 4e-3
+
+
+def test_dm256g_bit_equal_to_per_group(dev):
+    """4096 -> 11008 at b = 256 (43 output blocks: 3 groups, the multi-group kernel) == the
+    one-group kernel on each group's 16 (11) output blocks alone, bit for bit."""
+    from bcfft import ops
+    k, m, b, n = 4096, 11008, 256, 1000
+    torch.manual_seed(8)
+    c = (torch.randn(m // b, k // b, b, device=dev) * 0.01).to(torch.bfloat16)
+    x = torch.randn(n, k, device=dev).to(torch.bfloat16)
+    y = ops.forward(x, ops.spectra(c), None, b, m, algo="dft")
+    parts = []
+    for g0 in range(0, m // b, 16):
+        cg = c[g0:g0 + 16].contiguous()
+        parts.append(ops.forward(x, ops.spectra(cg), None, b, cg.shape[0] * b, algo="dft"))
+    assert torch.equal(y, torch.cat(parts, dim=1))

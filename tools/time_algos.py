@@ -86,7 +86,7 @@ if __name__ == "__main__":
         t_glu(b=64)
     if "--b256" in sys.argv:                        # the b = 256 sweep rows (bcfft_dm256.hip)
         shapes = [(4096, 4096, 256, "bf16", 8192), (4096, 11008, 256, "bf16", 8192), (11008, 4096, 256, "bf16", 8192),
-                  (11008, 4096, 256, "bf16", 1024), (11008, 4096, 256, "bf16", 64)]
+                  (4096, 11008, 256, "bf16", 1700), (11008, 4096, 256, "bf16", 1024), (11008, 4096, 256, "bf16", 64)]
     if "--down2" in sys.argv:
         shapes = [(11008, 4096, 128, "bf16", n) for n in (1700, 8192)]
     if "--smalln" in sys.argv:                      # AUTO's small-N crossover
