@@ -150,16 +150,21 @@ int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_featur
  * (32 * ceil(gate_blocks / 16), in_blocks, b): group g's 32 blocks are gate blocks [16g, 16g+16)
  * then up blocks [16g, 16g+16), zero past the last gate block (bcfft.ops.glu_weights builds it).
  *   x: (n_tokens, in_features), h: (n_tokens, gate_features), both x_dtype, 16-B aligned
- * Stationary geometries only (b = 128 with K = 4096: the DFT kernel, group g's gate blocks in its
- * first N-tile and up blocks in its second; b = 64 with K in {2048, 4096}: the stationary kernel),
- * else BCFFT_ERR_BLOCK; no bias (LLaMA's gate/up have none). Numerics follow torch on the reference's
- * tensors: gate and up rounded to x_dtype, silu(gate) rounded, the product rounded. */
+ * Geometries: b = 128 with K = 4096 (the DFT kernels, group g's gate blocks in its first N-tile
+ * and up blocks in its second; several groups with bf16 x: the multi-group kernel); b = 64 with
+ * K in {2048, 4096} (stationary kernel; bf16 x at K = 4096: the b = 64 DFT kernels); b = 256 with
+ * K = 4096 and bf16 x only (the b = 256 multi-group DFT kernel: each group split into 8 gate + 8
+ * up columns); else BCFFT_ERR_BLOCK. No bias (LLaMA's gate/up have none). Numerics follow torch
+ * on the reference's tensors: gate and up rounded to x_dtype, silu(gate) rounded, the product
+ * rounded. */
 int bcfft_forward_glu(const void* x, int x_dtype, int64_t n_tokens, int in_features, int gate_features,
                       int block_size, const void* spectra_gu, void* h, void* stream);
 
 /* bcfft_forward_glu with an engine choice: AUTO (bcfft_forward_glu) runs the DFT kernel at b = 128
- * with K = 4096 and the stationary kernel on the other stationary geometries; STAT, DFT and DFTX
- * force one (BCFFT_ERR_BLOCK where it does not serve the geometry; MFMA / VALU: BCFFT_ERR_ARG). */
+ * with K = 4096 (DFTX for fp32 x), the b = 64 DFT kernel for bf16 x at b = 64, K = 4096, the b = 256
+ * one for bf16 x at b = 256, K = 4096, and the stationary kernel on the other stationary
+ * geometries; STAT, DFT and DFTX force one (BCFFT_ERR_BLOCK where it does not serve the
+ * geometry; MFMA / VALU: BCFFT_ERR_ARG). */
 int bcfft_forward_glu_algo(const void* x, int x_dtype, int64_t n_tokens, int in_features, int gate_features,
                            int block_size, const void* spectra_gu, void* h, int algo, void* stream);
 

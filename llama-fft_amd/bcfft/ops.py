@@ -96,9 +96,12 @@ def forward_glu(x2d: torch.Tensor, spec_gu: torch.Tensor, block_size: int, gate_
     return h
 
 
-def glu_eligible(in_features: int, block_size: int) -> bool:
-    """Geometries the fused gate/up kernel serves (the stationary ones, include/bcfft.h)."""
+def glu_eligible(in_features: int, block_size: int, dtype: torch.dtype | None = None) -> bool:
+    """Geometries the fused gate/up kernel serves (include/bcfft.h): the stationary ones, and
+    b = 256 with K = 4096 for bf16 x (the b = 256 multi-group DFT kernel)."""
     n_in = in_features // block_size
+    if block_size == 256 and n_in == 16:
+        return dtype == torch.bfloat16
     return (block_size == 128 and n_in == 32) or (block_size == 64 and n_in in (32, 64))
 
 

@@ -1011,6 +1011,7 @@ constexpr int LDSG_BYTES = OSG_OFF + MAXG * NOB * 4;
 static_assert(LDSG_BYTES <= 160 * 1024, "LDS budget");
 }  // namespace d256
 
+template <bool GLU>
 __global__ __launch_bounds__(512, 2) void bc_forward_dm256g_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_out, const uint32_t* __restrict__ stat,
     const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
@@ -1026,7 +1027,11 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256g_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int n_groups = (n_out + NOB - 1) / NOB;
+  // GLU (fused gate/up + SwiGLU): n_out counts h blocks and the spectra hold ceil(n_out / 16)
+  // STAT groups of 16 gate + 16 up blocks (bcfft.ops.glu_weights). Virtual group v takes gate
+  // blocks 16 (v >> 1) + 8 (v & 1) + [0, 8) in output columns 0-7 and the matching up blocks in
+  // columns 8-15, so stage 3 pairs gate and up with one DPP row rotation and stores 8 h rows.
+  const int n_groups = GLU ? 2 * ((n_out + 15) / 16) : (n_out + NOB - 1) / NOB;
   const int64_t M = (int64_t)n_out * B;
   const int64_t n_mtiles = (n_tokens + TT - 1) / TT;
   const int64_t gstride = gridDim.x;
@@ -1063,10 +1068,16 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256g_kernel(
   };
   auto load_pass = [&](int g, int p, Breg& br) {
     const __amdgpu_buffer_rsrc_t brs = b_rsrc(g);
-    const int vo = opaque(lane) * 16;
+    const int ol = opaque(lane);
+    int vo;
+    if constexpr (GLU) {                            // column c of N-tile nt: lane c + 16 (lane >> 4)
+      const int o16 = ol & 15, h8 = 8 * (g & 1);
+      vo = (o16 < 8 ? 0 : 1024) + 16 * (h8 + (o16 & 7) + 16 * (ol >> 4));
+    } else {
+      vo = ol * 16 + (g & 1) * 1024;
+    }
 #pragma unroll
-    for (int j = 0; j < PF; ++j)
-      br[j] = __builtin_amdgcn_raw_buffer_load_b128(brs, vo, ((8 * p + j) * 2 + (g & 1)) * 1024, 0);
+    for (int j = 0; j < PF; ++j) br[j] = __builtin_amdgcn_raw_buffer_load_b128(brs, vo, (8 * p + j) * 2048, 0);
   };
 
   // ---- prologue: the first tile's x, the tables, every group's inverse weight scales, the first
@@ -1290,7 +1301,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256g_kernel(
     const int o16 = l & 15, g = l >> 4;
     char* slot = region + wave * SLOT;
     const int nmin = wsc[par * 16 + wave * 2];
-    const float ysc = __builtin_ldexpf(osl[grp * NOB + o16], 30 - nmin);
+    const int oidx = GLU ? 32 * (grp >> 1) + (o16 < 8 ? 8 * (grp & 1) + o16 : 16 + 8 * (grp & 1) + (o16 - 8))
+                         : grp * NOB + o16;
+    const float ysc = __builtin_ldexpf(osl[oidx], 30 - nmin);
     // Y fragments: B[k = 8 g + j][o] of virtual wave 4 ks + g, parity pr, spectrum s
     uint4 ye[2][2], yz[2][2], yw[2][2];
 #pragma unroll
@@ -1367,7 +1380,17 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256g_kernel(
           lo[r] = (e + o) * ysc;                    // y_t
           hi[r] = (e - o) * ysc;                    // y_{t+128}
         }
-        if (bias_dt != BCFFT_NONE) {                // .to(x dtype) :266, + bias :270-271
+        if constexpr (GLU) {                        // gate (columns 0-7) x up (8-15), torch's roundings
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            lo[r] = round_to(lo[r], XT);
+            hi[r] = round_to(hi[r], XT);
+            const float ulo = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(lo[r]), 0x128, 0xF, 0xF, false));
+            const float uhi = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(hi[r]), 0x128, 0xF, 0xF, false));
+            lo[r] = round_to(round_to(silu(lo[r]), XT) * ulo, XT);
+            hi[r] = round_to(round_to(silu(hi[r]), XT) * uhi, XT);
+          }
+        } else if (bias_dt != BCFFT_NONE) {         // .to(x dtype) :266, + bias :270-271
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             lo[r] = round_to(lo[r], XT);
@@ -1382,6 +1405,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256g_kernel(
             }
           }
         }
+        if (GLU && o16 >= 8) continue;              // GLU: the up columns stage nothing
         const int u = 4 * mt + g + 16 * hf;
         *reinterpret_cast<uint2*>(slot + 512 * o16 + 8 * (u ^ sw)) = make_uint2(pack16<XT>(lo[0], lo[1]), pack16<XT>(lo[2], lo[3]));
         *reinterpret_cast<uint2*>(slot + 512 * o16 + 8 * ((u + 32) ^ sw)) = make_uint2(pack16<XT>(hi[0], hi[1]), pack16<XT>(hi[2], hi[3]));
@@ -1391,18 +1415,20 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256g_kernel(
     // staged rows -> global: each instruction stores 1 KiB = 2 whole rows (32 lanes per row):
     // 16-B unit w of row r at physical 16-B unit w ^ r (the 8-B swizzle by 2 r keeps pairs)
     constexpr int RB = B * ESY;
+    constexpr int NQ = GLU ? 4 : 8;                 // 1 KiB stores: 2 rows each
+    const int64_t row0 = GLU ? 16 * (grp >> 1) + 8 * (grp & 1) : (int64_t)grp * NOB;
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
-        (char*)yv + (tok_ok ? tok : 0) * M * ESY + (int64_t)grp * NOB * RB, 0,
-        tok_ok ? (int)((M - (int64_t)grp * NOB * B) * ESY) : 0, 0x00020000);
+        (char*)yv + (tok_ok ? tok : 0) * M * ESY + row0 * RB, 0,
+        tok_ok ? (int)((M - row0 * B) * ESY) : 0, 0x00020000);
     const int w = l & 31, lr = l >> 5;
-    uint4 d[8];
+    uint4 d[NQ];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < NQ; ++q) {
       const int row = 2 * q + lr;
       d[q] = *reinterpret_cast<const uint4*>(slot + 512 * row + 16 * (w ^ row));
     }
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
+    for (int q = 0; q < NQ; ++q)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs, (2 * q + lr) * RB + 16 * w, 0, 0);
   };
 
@@ -1455,8 +1481,8 @@ void launch_forward_dm256(const void* x, int64_t n, int n_in, int n_out, const v
 #ifndef BCFFT_NO_DM256G
   if (n_in == d256::NI && groups >= 3 && groups <= d256::MAXG) {   // several groups: x transformed once
     const int64_t wgs = device_cu_count() < n_mtiles ? device_cu_count() : n_mtiles;
-    hipLaunchKernelGGL(bc_forward_dm256g_kernel, dim3((unsigned)wgs), dim3(512), 0, s, x, n, n_out, stat, osc, bias,
-                       bias_dt, y);
+    hipLaunchKernelGGL(bc_forward_dm256g_kernel<false>, dim3((unsigned)wgs), dim3(512), 0, s, x, n, n_out, stat, osc,
+                       bias, bias_dt, y);
     return;
   }
 #endif
@@ -1466,5 +1492,22 @@ void launch_forward_dm256(const void* x, int64_t n, int n_in, int n_out, const v
   else
     hipLaunchKernelGGL(bc_forward_dm256k_kernel, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat, osc,
                        bias, bias_dt, y);
+}
+}  // namespace bcfft
+
+namespace bcfft {
+// fused gate/up + SwiGLU at b = 256, K = 4096, bf16 (the multi-group kernel's GLU form): spec
+// holds ceil(n_gate / 16) STAT groups of 16 gate + 16 up blocks
+bool dm256_glu_eligible(int n_in, int b, int xdt) { return b == 256 && n_in == d256::NI && xdt == BCFFT_BF16; }
+
+void launch_forward_dm256_glu(const void* x, int64_t n, int n_gate, const void* spec, void* h, hipStream_t s) {
+  const int stat_groups = (n_gate + 15) / 16;
+  const SpecLayout sl = spec_layout(32 * stat_groups, d256::NI, 256);
+  const int64_t n_mtiles = (n + 7) / 8;
+  const int64_t wgs = device_cu_count() < n_mtiles ? device_cu_count() : n_mtiles;
+  const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
+  const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
+  hipLaunchKernelGGL(bc_forward_dm256g_kernel<true>, dim3((unsigned)wgs), dim3(512), 0, s, x, n, n_gate, stat, osc,
+                     nullptr, BCFFT_NONE, h);
 }
 }  // namespace bcfft

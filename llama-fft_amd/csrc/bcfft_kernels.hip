@@ -898,8 +898,18 @@ int bcfft_forward_glu_algo(const void* x, int x_dtype, int64_t n_tokens, int in_
     return BCFFT_ERR_SHAPE;
   if (!valid_dt(x_dtype)) return BCFFT_ERR_DTYPE;
   const int n_in = in_features / block_size, n_gate = gate_features / block_size;
-  if (!bcfft::stat_eligible(n_in, block_size))
+  const bool g256 = bcfft::dm256_glu_eligible(n_in, block_size, x_dtype);   // b = 256, K = 4096, bf16
+  if (!bcfft::stat_eligible(n_in, block_size) && !g256)
     return refuse("bcfft_forward_glu", algo, n_in, block_size, x_dtype, x_dtype);
+  if (g256) {
+    if (algo != BCFFT_ALGO_AUTO && algo != BCFFT_ALGO_DFT)
+      return refuse("bcfft_forward_glu", algo, n_in, block_size, x_dtype, x_dtype);
+    if (n_tokens == 0) return BCFFT_OK;
+    if (!x || !h || !spectra_gu) return BCFFT_ERR_ARG;
+    if (!aligned16(x) || !aligned16(h) || !aligned16(spectra_gu)) return BCFFT_ERR_ALIGN;
+    bcfft::launch_forward_dm256_glu(x, n_tokens, n_gate, spectra_gu, h, (hipStream_t)stream);
+    return record_launch();
+  }
   const bool dm = bcfft::dm_eligible(n_in, block_size);
   const bool dm64 = bcfft::dm64_eligible(n_in, block_size, x_dtype, false);   // h has x's dtype
   // AUTO: fp32 h takes the hi + lo products (DFTX), as bcfft_forward does for fp32 outputs

@@ -375,7 +375,7 @@ class BCFusedGateUp(nn.Module):
         # BCFFT_ALGO=mfma / valu asks for an exact engine, which has no fused form: two launches
         return (g.bias is None and u.bias is None and not grad and x.is_cuda
                 and _ops.default_algo() not in ("mfma", "valu")
-                and _ops.glu_eligible(g.in_features, g.block_size))
+                and _ops.glu_eligible(g.in_features, g.block_size, x.dtype))
 
     def _spectra(self) -> torch.Tensor:
         g, u = self._gate.c, self._up.c

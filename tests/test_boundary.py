@@ -84,6 +84,9 @@ def test_argument_validation_without_launch(built_lib):
     fa = lib.bcfft_forward_algo
     assert fa(fake, F32, 8, 4096, 4096, 128, fake, None, NONE, fake, F32, 9, None) == 6   # bad algo
     assert fa(None, F32, 0, 4096, 4096, 128, None, None, NONE, None, F32, 2, None) == 0
+    glu = lib.bcfft_forward_glu_algo
+    assert glu(fake, F32, 8, 4096, 11008, 256, fake, fake, 0, None) == 2      # b = 256 GLU: bf16 only
+    assert glu(fake, BF16, 8, 4096, 11008, 256, fake, fake, 3, None) == 2     # ... and no stationary form
     spec = lib.bcfft_spectra
     assert spec(fake, F32, 2, 2, 48, 0, fake, None) == 2
     assert spec(None, F32, 2, 2, 64, 0, fake, None) == 6

@@ -143,3 +143,40 @@ def test_dm256g_bit_equal_to_per_group(dev):
         cg = c[g0:g0 + 16].contiguous()
         parts.append(ops.forward(x, ops.spectra(cg), None, b, cg.shape[0] * b, algo="dft"))
     assert torch.equal(y, torch.cat(parts, dim=1))
+
+
+@pytest.mark.parametrize("n", [1, 37, 1700])
+def test_dm256_glu_matches_composition(dev, n):
+    """The fused gate/up + SwiGLU at b = 256 (bf16; virtual groups of 8 gate + 8 up blocks of the
+    multi-group kernel, paired by a DPP row rotation) against silu(gate) * up of the same
+    engine's two separate launches, and through the module path (BCFusedGateUp)."""
+    from bcfft import ops
+    torch.manual_seed(4)
+    k, m, b = 4096, 11008, 256
+    cg = torch.randn(m // b, k // b, b, device=dev) * 0.01
+    cu = torch.randn(m // b, k // b, b, device=dev) * 0.01
+    x = torch.randn(n, k, device=dev).to(torch.bfloat16)
+    assert ops.glu_eligible(k, b, torch.bfloat16) and not ops.glu_eligible(k, b, torch.float32)
+    h = ops.forward_glu(x, ops.spectra(ops.glu_weights(cg, cu)), b, m, algo="auto")
+    gt = ops.forward(x, ops.spectra(cg), None, b, m, algo="dft")
+    ut = ops.forward(x, ops.spectra(cu), None, b, m, algo="dft")
+    ref = (torch.nn.functional.silu(gt.float()).to(torch.bfloat16).float() * ut.float()).to(torch.bfloat16)
+    d = (h.float() - ref.float()).abs()
+    assert (d <= 2 * 2.0 ** -7 * ref.float().abs() + 1e-6).float().mean().item() > 0.999
+    assert ((h.float() - ref.float()).norm() / ref.float().norm()).item() < 4e-3
+
+
+def test_dm256_glu_module_path(dev):
+    """BCFusedGateUp at b = 256 bf16 takes the fused launch and matches the two modules."""
+    from patch_llama_fft import BCFusedGateUp, BlockCirculantLinear
+    torch.manual_seed(5)
+    g = BlockCirculantLinear(4096, 11008, block_size=256, bias=False).to(dev).to(torch.bfloat16).eval()
+    u = BlockCirculantLinear(4096, 11008, block_size=256, bias=False).to(dev).to(torch.bfloat16).eval()
+    f = BCFusedGateUp(g, u)
+    x = torch.randn(2, 50, 4096, device=dev).to(torch.bfloat16)
+    with torch.inference_mode():
+        assert f._fused_ok(x)
+        h = f(x)
+        ref = torch.nn.functional.silu(g(x)) * u(x)
+    assert h.shape == ref.shape
+    assert ((h.float() - ref.float()).norm() / ref.float().norm()).item() < 4e-3

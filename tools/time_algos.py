@@ -85,6 +85,7 @@ if __name__ == "__main__":
         shapes = [(4096, 4096, 64, "bf16", 8192), (4096, 11008, 64, "bf16", 8192), (4096, 11008, 64, "bf16", 1700)]
         t_glu(b=64)
     if "--b256" in sys.argv:                        # the b = 256 sweep rows (bcfft_dm256.hip)
+        t_glu(b=256)
         shapes = [(4096, 4096, 256, "bf16", 8192), (4096, 11008, 256, "bf16", 8192), (11008, 4096, 256, "bf16", 8192),
                   (4096, 11008, 256, "bf16", 1700), (11008, 4096, 256, "bf16", 1024), (11008, 4096, 256, "bf16", 64)]
     if "--down2" in sys.argv:
