@@ -273,12 +273,13 @@ def time_glu(dev, steps, k=4096, m=11008, b=128, n=8192, io="bf16"):
 
     with torch.inference_mode():
         fused = run(lambda: ops.forward_glu(x, sgu, b, m, algo="auto"))
-        fused_stat = run(lambda: ops.forward_glu(x, sgu, b, m, algo="stationary"))
+        fused_stat = run(lambda: ops.forward_glu(x, sgu, b, m, algo="stationary")) if b <= 128 else None
         unfused = run(lambda: torch.nn.functional.silu(ops.forward(x, sg, None, b, m)) * ops.forward(x, su, None, b, m))
     nbytes = n * k * SZ[io] + n * m * SZ[io] + 2 * (m // b) * (k // b) * (b // 2 + 1) * 8
     engine = "dft-glu" if resolved_kernel("auto", k, b, io)[0] in ("dft", "dftx") else "stationary-glu"
     return {"workload": f"gate/up {k}->{m} b={b} N={n} {io}-io + SwiGLU", "engine": engine,
-            "ms": round(fused, 4), "stationary_glu_ms": round(fused_stat, 4), "unfused_ms": round(unfused, 4),
+            "ms": round(fused, 4), "stationary_glu_ms": None if fused_stat is None else round(fused_stat, 4),
+            "unfused_ms": round(unfused, 4),
             "GB_s": round(nbytes / (fused * 1e-3) / 1e9, 1),
             "frac": round(nbytes / (fused * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
@@ -320,28 +321,25 @@ def run_variants(dev, algo, steps):
         vl = make_layer(vk, vm, vb, vio, False, dev)
         vx = torch.randn(vn, vk, device=dev).to(DT[vio])
         vw, vkern = time_layer(vl, vx, max(10, steps // 2), 5)
+        # the same forward replayed from a HIP graph (bcfft.graph), 10 forwards per graph: the
+        # GPU's time per launch whatever the host's per-call cost (eager back-to-back launches of
+        # a ~40 us kernel become host-bound on a busy host); this is the figure frac uses
+        from bcfft.graph import GraphedCall
+        g = GraphedCall(lambda t: vl(t), [vx], repeat=10)
         os.environ["BCFFT_ALGO"] = algo
+        gk = time_fn(g.replay, max(10, steps // 2), 3, None, dev)[1] / 10
+        del g
         vbytes = algo_bytes(vn, vk, vm, vb, vio, False)
-        entry = {"workload": f"{vk}->{vm} b={vb} N={vn} {vio}-io algo={va}",
-                 "engine": resolved_kernel(va, vk, vb, vio, vm)[1].replace("bc_forward_", "").replace("_kernel", ""),
-                 "ms": round(vkern, 4),
-                 "GTok_elem_s": round(vn * vm / (vkern * 1e-3) / 1e9, 3),
-                 "GB_s": round(vbytes / (vkern * 1e-3) / 1e9, 1),
-                 "frac": round(vbytes / (vkern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-        if vn <= 1024:
-            # launch-bound size: the same forward replayed from a HIP graph (bcfft.graph), 10
-            # forwards per graph, so the figure is the GPU's and not the host's per-call cost
-            from bcfft.graph import GraphedCall
-            os.environ["BCFFT_ALGO"] = va
-            g = GraphedCall(lambda t: vl(t), [vx], repeat=10)
-            os.environ["BCFFT_ALGO"] = algo
-            gk = time_fn(g.replay, max(10, steps // 2), 3, None, dev)[1] / 10
-            entry["graph_ms"] = round(gk, 4)
-            entry["graph_GB_s"] = round(vbytes / (gk * 1e-3) / 1e9, 1)
-            del g
-        variants.append(entry)
+        variants.append({"workload": f"{vk}->{vm} b={vb} N={vn} {vio}-io algo={va}",
+                         "engine": resolved_kernel(va, vk, vb, vio, vm)[1].replace("bc_forward_", "").replace("_kernel", ""),
+                         "ms": round(gk, 4),
+                         "eager_ms": round(vkern, 4),
+                         "GTok_elem_s": round(vn * vm / (gk * 1e-3) / 1e9, 3),
+                         "GB_s": round(vbytes / (gk * 1e-3) / 1e9, 1),
+                         "frac": round(vbytes / (gk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
         del vl, vx
-    variants.append(time_glu(dev, max(10, steps // 2)))
+    for gb in (128, 64, 256):                       # the fused gate/up at every block size of the sweep
+        variants.append(time_glu(dev, max(10, steps // 2), b=gb))
     return variants
 
 
