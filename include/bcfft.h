@@ -168,6 +168,29 @@ int bcfft_forward_glu(const void* x, int x_dtype, int64_t n_tokens, int in_featu
 int bcfft_forward_glu_algo(const void* x, int x_dtype, int64_t n_tokens, int in_features, int gate_features,
                            int block_size, const void* spectra_gu, void* h, int algo, void* stream);
 
+/* Fused BC-MLP: y = BC_down( silu(BC_gate(x)) * BC_up(x) ), the LLaMA MLP of
+ * patch_mlp_with_block_circulant (patch_llama_fft.py:343-394) as the reference times it
+ * (microbench_dense_vs_bc.py:183-188, `--bench_mlp`: bc_down(F.silu(bc_gate(x)) * bc_up(x))).
+ *   x, y: (n_tokens, hidden_features), x_dtype, 16-B aligned
+ *   spectra_gu:   bcfft_spectra of the interleaved gate/up weight (as bcfft_forward_glu's)
+ *   spectra_down: bcfft_spectra of the down weight (hidden/b x inter/b blocks)
+ * Modes:
+ *   FUSED: ONE launch (bcfft_dmm.hip). h never leaves the CU: its 180 MB HBM round trip at 8192
+ *          LLaMA-7B tokens disappears. Geometry: bf16, block_size 128, hidden 4096,
+ *          4096 < intermediate <= 127 * 128 (LLaMA-7B's 11008); else BCFFT_ERR_BLOCK. The output is
+ *          bit-identical to SPLIT's where SPLIT runs the 8-token streamed-weight down kernel.
+ *   SPLIT: bcfft_forward_glu into the caller's workspace (h), then bcfft_forward (AUTO engines).
+ *   AUTO:  FUSED where it serves the geometry, else SPLIT.
+ * workspace: bcfft_forward_mlp_workspace_bytes(...) bytes (0 for FUSED; may then be NULL). */
+enum bcfft_mlp_mode { BCFFT_MLP_AUTO = 0, BCFFT_MLP_FUSED = 1, BCFFT_MLP_SPLIT = 2 };
+
+int64_t bcfft_forward_mlp_workspace_bytes(int64_t n_tokens, int hidden_features, int inter_features, int block_size,
+                                          int x_dtype, int mode);
+
+int bcfft_forward_mlp(const void* x, int x_dtype, int64_t n_tokens, int hidden_features, int inter_features,
+                      int block_size, const void* spectra_gu, const void* spectra_down, void* y, int mode,
+                      void* workspace, int64_t workspace_bytes, void* stream);
+
 /* Loss-aware circulant projection of a dense weight. Replaces the per-block
  * Python loop of BlockCirculantLinear.from_linear (patch_llama_fft.py:207-219) over
  * dense_block_to_circulant_column_loss_aware (:82-128) with one launch:

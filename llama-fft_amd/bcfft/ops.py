@@ -96,6 +96,43 @@ def forward_glu(x2d: torch.Tensor, spec_gu: torch.Tensor, block_size: int, gate_
     return h
 
 
+def forward_mlp(x2d: torch.Tensor, spec_gu: torch.Tensor, spec_down: torch.Tensor, block_size: int,
+                inter_features: int, mode: str = "auto") -> torch.Tensor:
+    """y = BC_down(silu(BC_gate(x2d)) * BC_up(x2d)) (bcfft_forward_mlp): the LLaMA
+    MLP as microbench_dense_vs_bc.py:183-188 times it. spec_gu = spectra(glu_weights(c_gate,
+    c_up)), spec_down = spectra(c_down). mode "fused": one launch, h never written (bf16,
+    b = 128, hidden 4096, intermediate 4224..16256); "split": the gate/up + SwiGLU launch into a
+    workspace, then the down launch; "auto": fused where it applies. y has x2d's dtype and width."""
+    if mode not in _lib.MLP_MODES:
+        raise ValueError(f"bcfft.forward_mlp: mode {mode!r}, expected one of {sorted(_lib.MLP_MODES)}")
+    _lib.require_device(x2d, "bcfft.forward_mlp")
+    n, k = x2d.shape
+    b = block_size
+    if b > 0 and k % b == 0 and inter_features % b == 0:
+        _check_spectra(spec_gu, 32 * (-(-(inter_features // b) // 16)), k // b, b, "bcfft.forward_mlp")
+        _check_spectra(spec_down, k // b, inter_features // b, b, "bcfft.forward_mlp")
+    x2d = x2d.contiguous()
+    if x2d.data_ptr() % 16:
+        x2d = x2d.clone()
+    y = torch.empty((n, k), dtype=x2d.dtype, device=x2d.device)
+    lib = _lib.load()
+    code = _lib.MLP_MODES[mode]
+    ws_bytes = lib.bcfft_forward_mlp_workspace_bytes(n, k, inter_features, b, _lib.dtype_code(x2d.dtype), code)
+    ws = torch.empty(max(ws_bytes, 0), dtype=torch.uint8, device=x2d.device) if ws_bytes > 0 else None
+    _lib.check(lib.bcfft_forward_mlp(x2d.data_ptr(), _lib.dtype_code(x2d.dtype), n, k, inter_features, b,
+                                     spec_gu.data_ptr(), spec_down.data_ptr(), y.data_ptr(), code,
+                                     0 if ws is None else ws.data_ptr(), max(ws_bytes, 0),
+                                     _lib.stream_handle(x2d.device)), "bcfft_forward_mlp")
+    return y
+
+
+def mlp_fused_eligible(hidden_features: int, inter_features: int, block_size: int,
+                       dtype: torch.dtype | None = None) -> bool:
+    """Geometries of the one-launch BC-MLP kernel (bcfft_dmm.hip)."""
+    return (block_size == 128 and hidden_features == 4096 and inter_features % 128 == 0
+            and 32 < inter_features // 128 <= 127 and dtype in (None, torch.bfloat16))
+
+
 def glu_eligible(in_features: int, block_size: int, dtype: torch.dtype | None = None) -> bool:
     """Geometries the fused gate/up kernel serves (include/bcfft.h): the stationary ones, and
     b = 256 with K = 4096 for bf16 x (the b = 256 multi-group DFT kernel)."""

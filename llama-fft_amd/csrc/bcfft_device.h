@@ -602,6 +602,14 @@ bool dmk_eligible(int n_in, int b, int xdt, bool yf32);
 void launch_forward_dmk(const void* x, int64_t n, int n_in, int n_out, const void* spec, const void* bias,
                         int bias_dt, void* y, hipStream_t s);
 void launch_dmk_image(int n_out, int n_in, void* spec, hipStream_t s);
+// fused BC-MLP (bcfft_dmm.hip): y = down(silu(gate(x)) * up(x)) in one launch; bf16 x and y,
+// b = 128, hidden 4096 (n_in = n_out = 32 blocks), intermediate n_h blocks with 32 < n_h <= 127
+bool dmm_eligible(int n_in, int b, int xdt, int n_h, int n_out);
+#ifndef BCFFT_DMM_MIN_TOKENS
+#define BCFFT_DMM_MIN_TOKENS 1       // the MLP's AUTO mode takes the fused kernel from this many tokens
+#endif
+void launch_mlp_dmm(const void* x, int64_t n, int n_h, const void* spec_gu, const void* spec_dn, void* y,
+                    hipStream_t s);
 
 // weight prep (bcfft_prep.hip): loss-aware circulant projection of a dense (n_out*b, n_in*b)
 // weight into c (n_out, n_in, b) fp32; false for an unsupported block size

@@ -937,6 +937,69 @@ int bcfft_forward_glu(const void* x, int x_dtype, int64_t n_tokens, int in_featu
                                 BCFFT_ALGO_AUTO, stream);
 }
 
+// the fused BC-MLP's resolved mode: FUSED where bcfft_dmm.hip serves the geometry (AUTO: from
+// BCFFT_DMM_MIN_TOKENS tokens), else SPLIT; < 0 for invalid arguments
+static int mlp_mode(int64_t n_tokens, int hidden_features, int inter_features, int block_size, int x_dtype, int mode) {
+  if (mode != BCFFT_MLP_AUTO && mode != BCFFT_MLP_FUSED && mode != BCFFT_MLP_SPLIT) return -1;
+  if (!valid_block(block_size) || !valid_dt(x_dtype) || n_tokens < 0 || hidden_features <= 0 || inter_features <= 0 ||
+      hidden_features % block_size || inter_features % block_size)
+    return -1;
+  const int n_hid = hidden_features / block_size, n_h = inter_features / block_size;
+  const bool ok = bcfft::dmm_eligible(n_hid, block_size, x_dtype, n_h, n_hid);
+  if (mode == BCFFT_MLP_AUTO) return ok && n_tokens >= BCFFT_DMM_MIN_TOKENS ? BCFFT_MLP_FUSED : BCFFT_MLP_SPLIT;
+  return mode;
+}
+
+static int64_t dt_bytes(int dt) { return dt == BCFFT_F32 ? 4 : 2; }
+
+int64_t bcfft_forward_mlp_workspace_bytes(int64_t n_tokens, int hidden_features, int inter_features, int block_size,
+                                          int x_dtype, int mode) {
+  const int m = mlp_mode(n_tokens, hidden_features, inter_features, block_size, x_dtype, mode);
+  if (m < 0) return -1;
+  if (m == BCFFT_MLP_FUSED) return 0;
+  return (n_tokens * (int64_t)inter_features * dt_bytes(x_dtype) + 15) / 16 * 16;   // h
+}
+
+int bcfft_forward_mlp(const void* x, int x_dtype, int64_t n_tokens, int hidden_features, int inter_features,
+                      int block_size, const void* spectra_gu, const void* spectra_down, void* y, int mode,
+                      void* workspace, int64_t workspace_bytes, void* stream) {
+  g_last_detail[0] = 0;
+  if (mode != BCFFT_MLP_AUTO && mode != BCFFT_MLP_FUSED && mode != BCFFT_MLP_SPLIT) return BCFFT_ERR_ARG;
+  if (!valid_block(block_size)) return refuse("bcfft_forward_mlp", BCFFT_ALGO_AUTO, 0, block_size, x_dtype, x_dtype);
+  if (n_tokens < 0 || hidden_features <= 0 || inter_features <= 0 || hidden_features % block_size ||
+      inter_features % block_size)
+    return BCFFT_ERR_SHAPE;
+  if (!valid_dt(x_dtype)) return BCFFT_ERR_DTYPE;
+  const int n_hid = hidden_features / block_size, n_h = inter_features / block_size;
+  const int m = mlp_mode(n_tokens, hidden_features, inter_features, block_size, x_dtype, mode);
+  if (m == BCFFT_MLP_FUSED && !bcfft::dmm_eligible(n_hid, block_size, x_dtype, n_h, n_hid)) {
+    snprintf(g_last_detail, sizeof(g_last_detail),
+             "bcfft_forward_mlp: the fused kernel serves bf16, block_size 128, hidden 4096 and intermediate "
+             "4224..16256; got block_size %d, hidden %d, intermediate %d, x %s",
+             block_size, hidden_features, inter_features, dt_name(x_dtype));
+    return BCFFT_ERR_BLOCK;
+  }
+  if (n_tokens == 0) return BCFFT_OK;
+  if (!x || !y || !spectra_gu || !spectra_down) return BCFFT_ERR_ARG;
+  if (!aligned16(x) || !aligned16(y) || !aligned16(spectra_gu) || !aligned16(spectra_down) ||
+      (workspace && !aligned16(workspace)))
+    return BCFFT_ERR_ALIGN;
+  hipStream_t s = (hipStream_t)stream;
+  if (m == BCFFT_MLP_FUSED) {
+    bcfft::launch_mlp_dmm(x, n_tokens, n_h, spectra_gu, spectra_down, y, s);
+    return record_launch();
+  }
+  // SPLIT: h = silu(gate(x)) * up(x) into the workspace, then down(h) (two launches, AUTO engines)
+  const int64_t need = bcfft_forward_mlp_workspace_bytes(n_tokens, hidden_features, inter_features, block_size,
+                                                         x_dtype, BCFFT_MLP_SPLIT);
+  if (!workspace || workspace_bytes < need) return BCFFT_ERR_ARG;
+  int st = bcfft_forward_glu(x, x_dtype, n_tokens, hidden_features, inter_features, block_size, spectra_gu, workspace,
+                             stream);
+  if (st != BCFFT_OK) return st;
+  return bcfft_forward(workspace, x_dtype, n_tokens, inter_features, hidden_features, block_size, spectra_down,
+                       nullptr, BCFFT_NONE, y, x_dtype, stream);
+}
+
 int bcfft_forward(const void* x, int x_dtype, int64_t n_tokens, int in_features,
                   int out_features, int block_size, const void* spectra, const void* bias,
                   int bias_dtype, void* y, int y_dtype, void* stream) {

@@ -194,3 +194,33 @@ def test_refusal_names_engine_and_geometry(built_lib):
         _lib.check(st, "bcfft_forward")
     assert lib.bcfft_forward_ws(None, F32, 0, 4096, 4096, 128, None, None, NONE, None, F32, 0, None, 0, None) == 0
     assert lib.bcfft_last_error_detail().decode() == ""
+
+
+def test_mlp_mode_and_workspace_without_gpu(built_lib):
+    """bcfft_forward_mlp's mode resolution is host logic: the one-launch kernel (no workspace) for
+    bf16 at b = 128, hidden 4096, intermediate 33..127 blocks; the split form's workspace is h;
+    a forced FUSED on another geometry is refused with its reason before any launch."""
+    from bcfft import _lib
+    lib = _lib.load()
+    wb = lib.bcfft_forward_mlp_workspace_bytes
+    AUTO, FUSED, SPLIT = (_lib.MLP_MODES[m] for m in ("auto", "fused", "split"))
+    F32, BF16 = _lib.BCFFT_F32, _lib.BCFFT_BF16
+    assert wb(8192, 4096, 11008, 128, BF16, AUTO) == 0
+    assert wb(1, 4096, 11008, 128, BF16, FUSED) == 0
+    assert wb(8192, 4096, 11008, 128, BF16, SPLIT) == 8192 * 11008 * 2
+    assert wb(7, 4096, 11008, 128, F32, AUTO) == (7 * 11008 * 4 + 15) // 16 * 16   # fp32: split
+    assert wb(5, 4096, 11008, 64, BF16, AUTO) == 5 * 11008 * 2                      # b = 64: split
+    assert wb(5, 4096, 4096, 128, BF16, AUTO) == 5 * 4096 * 2                       # 32 h blocks: split
+    assert wb(5, 4096, 16384, 128, BF16, AUTO) == 5 * 16384 * 2                     # 128 h blocks: split
+    assert wb(5, 4096, 16256, 128, BF16, AUTO) == 0                                 # 127 h blocks
+    assert wb(5, 4096, 11008, 128, BF16, 3) == -1
+    assert wb(5, 4000, 11008, 128, BF16, AUTO) == -1
+    fake = 4096
+    fm = lib.bcfft_forward_mlp
+    assert fm(fake, F32, 8, 4096, 11008, 128, fake, fake, fake, FUSED, None, 0, None) == 2
+    d = lib.bcfft_last_error_detail().decode()
+    assert "bcfft_forward_mlp" in d and "x fp32" in d and "intermediate 11008" in d, d
+    assert fm(fake, BF16, 8, 4096, 11008, 128, fake, fake, fake, SPLIT, None, 0, None) == 6   # no workspace
+    assert fm(fake, BF16, 8, 4096, 11008, 128, fake, fake, fake + 2, FUSED, None, 0, None) == 4   # y misaligned
+    assert fm(None, BF16, 0, 4096, 11008, 128, None, None, None, AUTO, None, 0, None) == 0
+    assert fm(fake, BF16, 8, 4096, 11008, 128, fake, fake, fake, 7, None, 0, None) == 6

@@ -1,0 +1,154 @@
+"""GPU parity of the fused BC-MLP (bcfft_forward_mlp): y = down(silu(gate(x)) *
+up(x)) in one launch (bcfft_dmm.hip), the unit the reference times with `--bench_mlp`
+(src/microbench_dense_vs_bc.py:183-188) and the MLP of patch_mlp_with_block_circulant
+(patch_llama_fft.py:343-394).
+
+* Against the split form (the gate/up + SwiGLU launch, h in HBM, then the down launch): every
+  rounding is the same, so the outputs must be BIT-IDENTICAL (torch.equal). That covers ragged
+  token counts, partial last gate/up groups (the down projection's partial last K-chunk), chunks
+  of very different magnitude (the down kernel's reference-exponent rescale), zero tokens, and
+  the full 8192-token LLaMA-7B shape.
+* Against the CPU oracle (oracle/bc_oracle.py: the reference's fp32 FFT forward per projection,
+  bf16 roundings where torch rounds): 16-bit output bounds as the GLU tests use."""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import rel_err
+from oracle import bc_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+B = 128
+HID = 4096
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    import bcfft
+    bcfft.load()
+    return torch.device("cuda:0")
+
+
+def _weights(dev, n_h, seed, chunk_gain=None):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    cg = torch.randn(n_h, HID // B, B, generator=g) * 0.01
+    cu = torch.randn(n_h, HID // B, B, generator=g) * 0.01
+    cd = torch.randn(HID // B, n_h, B, generator=g) * 0.01
+    if chunk_gain is not None:                       # h chunk k (16 blocks) scaled by chunk_gain[k]
+        for k, s in enumerate(chunk_gain):
+            cu[16 * k:16 * k + 16] *= s
+    return cg.to(dev), cu.to(dev), cd.to(dev)
+
+
+def _run(dev, x, cg, cu, cd, mode):
+    from bcfft import ops
+    n_h = cg.shape[0]
+    sgu = ops.spectra(ops.glu_weights(cg, cu))
+    sd = ops.spectra(cd)
+    y = ops.forward_mlp(x, sgu, sd, B, n_h * B, mode=mode)
+    torch.cuda.synchronize()
+    return y
+
+
+def _silu(a):
+    return a / (1.0 + np.exp(-a.astype(np.float64)))
+
+
+def oracle_mlp(x, cg, cu, cd, dt=O.BF16):
+    xr = O.round_to(x, dt)
+    gt = O.bc_forward(xr, cg, x_dtype=dt)
+    ut = O.bc_forward(xr, cu, x_dtype=dt)
+    s = O.round_to(_silu(gt).astype(np.float32), dt)
+    h = O.round_to((s.astype(np.float64) * ut).astype(np.float32), dt)
+    return O.bc_forward(h, cd, x_dtype=dt)
+
+
+@pytest.mark.parametrize("n,n_h", [(1, 86), (5, 86), (8, 86), (9, 86), (37, 86), (300, 86),
+                                   (16, 96), (23, 33), (19, 127), (2048, 86)])
+def test_fused_equals_split(dev, n, n_h):
+    torch.manual_seed(n + n_h)
+    cg, cu, cd = _weights(dev, n_h, seed=n_h)
+    x = torch.randn(n, HID, device=dev).to(torch.bfloat16)
+    yf = _run(dev, x, cg, cu, cd, "fused")
+    ys = _run(dev, x, cg, cu, cd, "split")
+    assert yf.shape == (n, HID) and yf.dtype == torch.bfloat16
+    assert torch.isfinite(yf.float()).all()
+    diff = (yf.float() - ys.float()).abs().max().item()
+    assert torch.equal(yf, ys), f"fused != split (max |diff| {diff:.3e})"
+
+
+def test_fused_equals_split_loud_quiet_chunks_and_zero_tokens(dev):
+    """h chunks 1e3 louder / 1e-3 quieter than the first (the down kernel lowers a token's
+    reference exponent and rescales its accumulators), plus all-zero and tiny tokens."""
+    gains = [1.0, 1e3, 1e-3, 1.0, 30.0, 1e-2]
+    cg, cu, cd = _weights(dev, 86, seed=5, chunk_gain=gains)
+    torch.manual_seed(5)
+    x = torch.randn(45, HID, device=dev)
+    x[3] = 0
+    x[10] *= 1e-6
+    x[20, :2048] = 0
+    x = x.to(torch.bfloat16)
+    yf = _run(dev, x, cg, cu, cd, "fused")
+    ys = _run(dev, x, cg, cu, cd, "split")
+    assert torch.equal(yf, ys)
+    assert (yf[3] == 0).all()
+
+
+def test_fused_vs_oracle(dev):
+    n, n_h = 37, 86
+    cg, cu, cd = _weights(dev, n_h, seed=11)
+    torch.manual_seed(11)
+    x = torch.randn(n, HID, device=dev).to(torch.bfloat16)
+    y = _run(dev, x, cg, cu, cd, "fused").float().cpu().numpy()
+    ref = oracle_mlp(x.float().cpu().numpy(), cg.cpu().numpy(), cu.cpu().numpy(), cd.cpu().numpy())
+    e = rel_err(y, ref)
+    # bf16 output (2^-8 relative rounding), the fp16 weight spectra of both BC stages (~4e-4 each)
+    # carried through SiLU, and the bf16 rounding of h feeding the down projection
+    assert e < 4e-3, f"rel err {e:.3e}"
+    rms = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
+    assert np.max(np.abs(y - ref)) < 8 * 2.0 ** -7 * rms + 2 * 2.0 ** -7 * np.max(np.abs(ref))
+
+
+def test_fused_full_size_llama7b(dev):
+    """8192 tokens, 4096 -> 11008 -> 4096 (the reference's --bench_mlp shape at batch 4 x seq 2048):
+    against the split form bit for bit (the split form's down launch takes 16-token tiles here),
+    and the first 24 tokens against the oracle."""
+    n, n_h = 8192, 86
+    cg, cu, cd = _weights(dev, n_h, seed=21)
+    torch.manual_seed(21)
+    x = torch.randn(n, HID, device=dev).to(torch.bfloat16)
+    yf = _run(dev, x, cg, cu, cd, "fused")
+    ys = _run(dev, x, cg, cu, cd, "split")
+    assert torch.isfinite(yf.float()).all()
+    d = (yf.float() - ys.float())
+    assert torch.equal(yf, ys), (f"max |diff| {d.abs().max().item():.3e}, rel "
+                                 f"{(d.norm() / ys.float().norm()).item():.3e}")
+    ref = oracle_mlp(x[:24].float().cpu().numpy(), cg.cpu().numpy(), cu.cpu().numpy(), cd.cpu().numpy())
+    assert rel_err(yf[:24].float().cpu().numpy(), ref) < 4e-3
+
+
+def test_auto_and_ineligible(dev):
+    """AUTO: one launch on the fused geometry; fp32 x and b = 64 run the split form; a forced
+    fused launch on them raises with the reason."""
+    from bcfft import ops
+    cg, cu, cd = _weights(dev, 86, seed=3)
+    x = torch.randn(11, HID, device=dev)
+    ya = _run(dev, x.to(torch.bfloat16), cg, cu, cd, "auto")
+    yf = _run(dev, x.to(torch.bfloat16), cg, cu, cd, "fused")
+    assert torch.equal(ya, yf)
+    y32 = _run(dev, x, cg, cu, cd, "auto")
+    assert y32.dtype == torch.float32
+    ref = oracle_mlp(x.cpu().numpy(), cg.cpu().numpy(), cu.cpu().numpy(), cd.cpu().numpy(), O.F32)
+    assert rel_err(y32.cpu().numpy(), ref) < 1e-3
+    with pytest.raises(RuntimeError, match="intermediate 11008"):
+        _run(dev, x, cg, cu, cd, "fused")
+    c64g = torch.randn(44, 32, 64, device=dev) * 0.01
+    c64d = torch.randn(32, 44, 64, device=dev) * 0.01
+    x64 = torch.randn(6, 2048, device=dev).to(torch.bfloat16)
+    y64 = ops.forward_mlp(x64, ops.spectra(ops.glu_weights(c64g, c64g)), ops.spectra(c64d), 64, 44 * 64)
+    h = ops.forward_glu(x64, ops.spectra(ops.glu_weights(c64g, c64g)), 64, 44 * 64)
+    y64r = ops.forward(h, ops.spectra(c64d), None, 64, 2048)
+    # the C ABI's split form runs the down launch unsplit; ops.forward may split K at this size
+    assert ((y64.float() - y64r.float()).norm() / y64r.float().norm()).item() < 2e-3
