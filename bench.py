@@ -284,6 +284,40 @@ def time_glu(dev, steps, k=4096, m=11008, b=128, n=8192, io="bf16"):
             "frac": round(nbytes / (fused * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
+def time_mlp(dev, steps, k=4096, m=11008, b=128, n=8192):
+    """The whole BC-MLP down(silu(gate(x)) * up(x)) (microbench_dense_vs_bc.py:183-188, the
+    reference's --bench_mlp unit): ONE launch (bcfft_forward_mlp FUSED, h never
+    written) vs the split form (gate/up + SwiGLU launch, h in HBM, down launch). bf16."""
+    from bcfft import ops
+    torch.manual_seed(4)
+    cg = torch.randn(m // b, k // b, b, device=dev) * 0.01
+    cu = torch.randn(m // b, k // b, b, device=dev) * 0.01
+    cd = torch.randn(k // b, m // b, b, device=dev) * 0.01
+    x = torch.randn(n, k, device=dev).to(torch.bfloat16)
+    sgu, sd = ops.spectra(ops.glu_weights(cg, cu)), ops.spectra(cd)
+
+    def run(fn):
+        for _ in range(5):
+            fn()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(steps):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / steps
+
+    with torch.inference_mode():
+        fused = run(lambda: ops.forward_mlp(x, sgu, sd, b, m, mode="fused"))
+        split = run(lambda: ops.forward_mlp(x, sgu, sd, b, m, mode="split"))
+    nbytes = 2 * n * k * 2                          # x + y (the weights stream from L2)
+    return {"workload": f"MLP {k}->{m}->{k} b={b} N={n} bf16-io (gate/up + SwiGLU + down)",
+            "engine": "mlp_dmm (one launch)", "ms": round(fused, 4), "split_ms": round(split, 4),
+            "GTok_s": round(n / (fused * 1e-3) / 1e9, 4),
+            "xy_GB_s": round(nbytes / (fused * 1e-3) / 1e9, 1)}
+
+
 def load_traffic(tag, kernel, algo=None):
     """Per-launch HBM bytes of this kernel and engine on this workload from the newest
     profiles/pmc_traffic_*.json that measured that triple (None if none did; tools/pmc_traffic.py
@@ -340,6 +374,7 @@ def run_variants(dev, algo, steps):
         del vl, vx
     for gb in (128, 64, 256):                       # the fused gate/up at every block size of the sweep
         variants.append(time_glu(dev, max(10, steps // 2), b=gb))
+    variants.append(time_mlp(dev, max(10, steps // 2)))
     return variants
 
 

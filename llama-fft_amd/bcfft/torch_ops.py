@@ -8,6 +8,8 @@ a host tensor fails loudly as in bcfft.ops.
 
     torch.ops.bcfft.forward(x2d, spec, bias, block_size, out_features, algo) -> y
     torch.ops.bcfft.spectra(c, transpose_conj) -> spec
+    torch.ops.bcfft.forward_glu(x2d, spec_gu, block_size, gate_features, algo) -> h
+    torch.ops.bcfft.forward_mlp(x2d, spec_gu, spec_down, block_size, inter_features, mode) -> y
 """
 from __future__ import annotations
 
@@ -49,9 +51,39 @@ def _spectra_fake(c, transpose_conj=False):
     return c.new_empty((ops.spectra_numel(n_out, n_in, b),), dtype=torch.float32)
 
 
+@torch.library.custom_op("bcfft::forward_glu", mutates_args=())
+def forward_glu(x2d: torch.Tensor, spec_gu: torch.Tensor, block_size: int, gate_features: int,
+                algo: str = "auto") -> torch.Tensor:
+    """h = silu(BC_gate(x2d)) * BC_up(x2d): bcfft.ops.forward_glu (the patched LLaMA MLP's inner
+    product, patch_llama_fft.py:343-394)."""
+    return ops.forward_glu(x2d, spec_gu, block_size, gate_features, algo=algo)
+
+
+@forward_glu.register_fake
+def _forward_glu_fake(x2d, spec_gu, block_size, gate_features, algo="auto"):
+    if x2d.dim() != 2 or block_size <= 0 or x2d.shape[1] % block_size or gate_features % block_size:
+        raise ValueError("bcfft::forward_glu: x2d must be (N, in_features), features multiples of block_size")
+    return x2d.new_empty((x2d.shape[0], gate_features))
+
+
+@torch.library.custom_op("bcfft::forward_mlp", mutates_args=())
+def forward_mlp(x2d: torch.Tensor, spec_gu: torch.Tensor, spec_down: torch.Tensor, block_size: int,
+                inter_features: int, mode: str = "auto") -> torch.Tensor:
+    """y = BC_down(silu(BC_gate(x2d)) * BC_up(x2d)): bcfft.ops.forward_mlp (SURVEY.md §8 f4;
+    microbench_dense_vs_bc.py:183-188)."""
+    return ops.forward_mlp(x2d, spec_gu, spec_down, block_size, inter_features, mode=mode)
+
+
+@forward_mlp.register_fake
+def _forward_mlp_fake(x2d, spec_gu, spec_down, block_size, inter_features, mode="auto"):
+    if x2d.dim() != 2 or block_size <= 0 or x2d.shape[1] % block_size or inter_features % block_size:
+        raise ValueError("bcfft::forward_mlp: x2d must be (N, hidden), features multiples of block_size")
+    return x2d.new_empty(x2d.shape)
+
+
 def registered() -> bool:
     """True once the ops are visible under torch.ops.bcfft (importing this module registers them)."""
-    return hasattr(torch.ops.bcfft, "forward") and hasattr(torch.ops.bcfft, "spectra")
+    return all(hasattr(torch.ops.bcfft, n) for n in ("forward", "spectra", "forward_glu", "forward_mlp"))
 
 
-__all__ = ["forward", "spectra", "registered", "_lib"]
+__all__ = ["forward", "spectra", "forward_glu", "forward_mlp", "registered", "_lib"]

@@ -394,14 +394,36 @@ class BCFusedGateUp(nn.Module):
         return h.view(*shape[:-1], self._gate.out_features)
 
 
+def _mlp_fused_ok(mlp, x: torch.Tensor) -> bool:
+    """The whole MLP as ONE launch (bcfft_forward_mlp) when down_proj is BC too,
+    without bias or autograd, on the fused kernel's geometry (bf16, b = 128, hidden 4096)."""
+    gu, d = mlp._bc_gate_up, mlp.down_proj
+    if not isinstance(d, BlockCirculantLinear) or d.bias is not None or not gu._fused_ok(x):
+        return False
+    if torch.is_grad_enabled() and d.c.requires_grad:
+        return False
+    g = gu._gate
+    return (d.block_size == g.block_size and d.in_features == g.out_features and d.out_features == g.in_features
+            and _ops.default_algo() in ("auto", "dft")
+            and _ops.mlp_fused_eligible(d.out_features, d.in_features, d.block_size, x.dtype))
+
+
 def _fused_mlp_forward(self, x):
+    if _mlp_fused_ok(self, x):
+        gu, d = self._bc_gate_up, self.down_proj
+        shape = x.shape
+        x2d = gu._gate._flatten(x)
+        y = _ops.forward_mlp(x2d, gu._spectra(), d._spectra(d.c), d.block_size, d.in_features)
+        return y.view(*shape[:-1], d.out_features)
     return self.down_proj(self._bc_gate_up(x))
 
 
 def fuse_mlp_gate_up(model) -> int:
     """Route each decoder MLP whose gate_proj and up_proj are BlockCirculantLinear (same shape,
     act = SiLU, as patch_mlp_with_block_circulant leaves them) through BCFusedGateUp: its
-    forward becomes down_proj(silu(gate(x)) * up(x)) with the fused launch. Parameters and
+    forward becomes down_proj(silu(gate(x)) * up(x)) with the fused launch. When down_proj is
+    BlockCirculantLinear too and the geometry allows it (bf16, b = 128, hidden 4096), the whole
+    MLP runs as ONE launch (bcfft_forward_mlp: h never leaves the CU). Parameters and
     state_dict are unchanged. Returns the number of MLPs rewired."""
     import types
     n = 0

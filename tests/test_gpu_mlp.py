@@ -152,3 +152,41 @@ def test_auto_and_ineligible(dev):
     y64r = ops.forward(h, ops.spectra(c64d), None, 64, 2048)
     # the C ABI's split form runs the down launch unsplit; ops.forward may split K at this size
     assert ((y64.float() - y64r.float()).norm() / y64r.float().norm()).item() < 2e-3
+
+
+def test_llama_mlp_module_runs_one_launch(dev):
+    """fuse_mlp_gate_up on a one-layer LLaMA-7B-width model (hidden 4096, intermediate 11008,
+    every projection BC at b = 128, bf16): the MLP forward is the one-launch kernel, equal to its
+    own two-launch composition bit for bit, and the logits match the unfused model."""
+    transformers = pytest.importorskip("transformers")
+    import patch_llama_fft as P
+    torch.manual_seed(0)
+    cfg = transformers.LlamaConfig(hidden_size=4096, intermediate_size=11008, num_hidden_layers=1,
+                                   num_attention_heads=32, num_key_value_heads=32, vocab_size=256,
+                                   max_position_embeddings=64)
+    model = transformers.LlamaForCausalLM(cfg).to(dev).to(torch.bfloat16).eval()
+    P.patch_linear_with_block_circulant(model, num_layers_to_patch=1, block_size=128)   # c stays fp32
+    ids = torch.randint(0, 256, (2, 16), device=dev)
+    mlp = model.model.layers[0].mlp
+    x = torch.randn(2, 16, 4096, device=dev).to(torch.bfloat16)
+    with torch.no_grad():
+        ref = model(input_ids=ids).logits.float()
+        assert P.fuse_mlp_gate_up(model) == 1
+        assert P._mlp_fused_ok(mlp, x)
+        y1 = mlp(x)
+        y2 = mlp.down_proj(mlp._bc_gate_up(x))
+        out = model(input_ids=ids).logits.float()
+    assert torch.equal(y1, y2)
+    assert ((out - ref).norm() / ref.norm()).item() < 2e-2
+
+
+def test_torch_op_forward_mlp(dev):
+    import bcfft.torch_ops  # noqa: F401
+    from bcfft import ops
+    cg, cu, cd = _weights(dev, 86, seed=8)
+    x = torch.randn(13, HID, device=dev).to(torch.bfloat16)
+    sgu, sd = ops.spectra(ops.glu_weights(cg, cu)), ops.spectra(cd)
+    y = torch.ops.bcfft.forward_mlp(x, sgu, sd, B, 86 * B, "auto")
+    assert torch.equal(y, ops.forward_mlp(x, sgu, sd, B, 86 * B))
+    torch.library.opcheck(torch.ops.bcfft.forward_mlp.default, (x, sgu, sd, B, 86 * B, "fused"),
+                          test_utils=("test_schema", "test_faketensor"))

@@ -43,3 +43,25 @@ def test_real_op_refuses_host_tensors():
     import bcfft.torch_ops  # noqa: F401
     with pytest.raises(RuntimeError, match="ROCm device"):
         torch.ops.bcfft.forward(torch.zeros(2, 128), torch.zeros(10), None, 64, 128, "auto")
+
+
+def test_glu_and_mlp_fake_shapes():
+    import bcfft.torch_ops  # noqa: F401
+    from bcfft import ops
+    b, h, f = 128, 4096, 11008
+    with FakeTensorMode():
+        x = torch.empty(21, h, dtype=torch.bfloat16)
+        sgu = torch.empty(ops.spectra_numel(32 * 6, h // b, b), dtype=torch.float32)
+        sd = torch.empty(ops.spectra_numel(h // b, f // b, b), dtype=torch.float32)
+        hh = torch.ops.bcfft.forward_glu(x, sgu, b, f, "auto")
+        assert hh.shape == (21, f) and hh.dtype == torch.bfloat16
+        y = torch.ops.bcfft.forward_mlp(x, sgu, sd, b, f, "auto")
+        assert y.shape == (21, h) and y.dtype == torch.bfloat16
+        with pytest.raises(ValueError):
+            torch.ops.bcfft.forward_mlp(torch.empty(3, 1000), sgu, sd, b, f, "auto")
+
+
+def test_real_mlp_op_refuses_host_tensors():
+    import bcfft.torch_ops  # noqa: F401
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        torch.ops.bcfft.forward_mlp(torch.zeros(2, 4096), torch.zeros(10), torch.zeros(10), 128, 11008, "auto")
