@@ -20,7 +20,8 @@
 //        scale with 2^HEAD headroom), in place;
 //      - down stage 2 of chunk g for all 8 tokens on the wave's 8 bins, accumulating over the
 //        chunks in 64 VGPRs (the reference-exponent alignment of bcfft_dmk.hip).
-//  * Tile end: the down accumulators as Y units into WR, stage 3 of token w, y stores.
+//  * Tile end: the down accumulators as Y units into WR; their stage 3 (token w) and y stores run
+//    beside the next tile's gate/up stage 1.
 //
 // One 64-register buffer carries every B fragment, in the order they are consumed: gate/up
 // K-step 0 of group g, K-step 1 of g, down chunk g, gate/up K-step 0 of g + 1, ... Each fragment
@@ -33,7 +34,7 @@
 // bcfft_dmk.hip<8>) in the same order: h is rounded to bf16 where the two-launch path stores it,
 // so the fused output is bit-identical to it (tests/test_gpu_mlp.py checks this).
 //
-// LDS (149,888 B): XR and WR, each 8 token slots of 8,256 B (64 B off the 256-B bank period, as
+// LDS (149,760 B): XR and WR, each 8 token slots of 8,256 B (64 B off the 256-B bank period, as
 // in bcfft_dm8.hip), the DFT table, the scale exponents, the inverse weight scales.
 #include "bcfft_device.h"
 #include "bcfft_dm_table.h"
@@ -663,11 +664,15 @@ __global__ __launch_bounds__(512, 2) void bc_mlp_dmm_kernel(
   //                gate/up stage 3 of token w (h chunk into WR slot w); down stage 1    | Bd |
   //                down stage 2 of chunk g (bb -> gate/up K-step 0 of the next group)   | Be |
   //   down Y units into WR                                                             | Bf |
-  //   down stage 3 of token w, y stores (the next tile's Ba orders WR's reuse)
+  // and the tile's down stage 3 (token w, y stores) runs beside the NEXT tile's stage 1: they
+  // touch different regions (WR / XR), and that tile's Ba orders WR's reuse (bcfft_dmk.hip's
+  // deferred stage 3)
+  int64_t mprev = -1;
   for (int64_t m = m0; m < n_mtiles; m += gstride) {
     const bool more_tiles = m + gstride < n_mtiles;
     wait_vmcnt<0>();                                // x(m), and the first group's fragments
     gu_stage1();
+    if (mprev >= 0) dn_stage3(mprev * TT + wave);
     lds_barrier();                                  // Ba: X units and exponents complete
     gu_factors();
     for (int g = 0; g < n_groups; ++g) {
@@ -684,8 +689,9 @@ __global__ __launch_bounds__(512, 2) void bc_mlp_dmm_kernel(
     }
     dn_ywrite();
     lds_barrier();                                  // Bf: Y units and reference exponents
-    dn_stage3(m * TT + wave);
+    mprev = m;
   }
+  dn_stage3(mprev * TT + wave);                     // the last tile's (every workgroup has one)
 }
 
 bool dmm_eligible(int n_in, int b, int xdt, int n_h, int n_out) {

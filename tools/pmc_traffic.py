@@ -15,7 +15,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("bc_forward_dm_kernel", "bc_forward_dm8_kernel", "bc_forward_dmk_kernel", "bc_forward_dm64_kernel",
+KERNELS = ("bc_mlp_dmm_kernel", "bc_forward_dm_kernel", "bc_forward_dm8_kernel", "bc_forward_dmk_kernel", "bc_forward_dm64_kernel",
            "bc_forward_dmg_kernel", "bc_forward_dm256_kernel", "bc_forward_dm256k_kernel", "bc_forward_dm64k_kernel", "bc_forward_dm64g_kernel", "bc_forward_dm256g_kernel",
            "bc_forward_stat_kernel", "bc_forward_mfma_kernel", "bc_forward_valu_kernel")
 
