@@ -180,7 +180,9 @@ int bcfft_forward_glu_algo(const void* x, int x_dtype, int64_t n_tokens, int in_
  *          4096 < intermediate <= 127 * 128 (LLaMA-7B's 11008); else BCFFT_ERR_BLOCK. The output is
  *          bit-identical to SPLIT's where SPLIT runs the 8-token streamed-weight down kernel.
  *   SPLIT: bcfft_forward_glu into the caller's workspace (h), then bcfft_forward (AUTO engines).
- *   AUTO:  FUSED where it serves the geometry, else SPLIT.
+ *   AUTO:  FUSED where it serves the geometry and its 8-token tiles fill at least 3/8 of the CUs
+ *          (N >= 768 on MI355X's 256), else SPLIT (at small N the split form's per-group gate/up
+ *          kernel spreads over more CUs: 34 vs 52.6 us at N = 256).
  * workspace: bcfft_forward_mlp_workspace_bytes(...) bytes (0 for FUSED; may then be NULL). */
 enum bcfft_mlp_mode { BCFFT_MLP_AUTO = 0, BCFFT_MLP_FUSED = 1, BCFFT_MLP_SPLIT = 2 };
 

@@ -569,6 +569,15 @@ bool dm8_eligible(int n_in, int b, int xdt, bool yf32);
 // several output groups at bf16 I/O (bcfft_dmg.hip): one workgroup runs a token tile's stage 1
 // once and loops over the groups with their weight fragments streamed from L2
 bool dmg_eligible(int n_in, int b, int xdt, bool yf32, int n_out, bool glu);
+// The multi-group kernels give one workgroup an 8-token tile for ALL its output groups, so a
+// launch has only ceil(N / 8) workgroups; the per-group kernels spread (tile, group) pairs over
+// the CUs. Measured at b = 128, bf16 (profiles/r03h_dmg_switch.log, 256 CUs): 4096 -> 11008 and
+// fused q/k/v pay from 96 tiles (N = 768: 18.2 vs 18.9 us; N = 20: 15.6 vs 9.7 us), the fused
+// gate/up + SwiGLU from ~160 tiles (N = 1024: 38.7 vs 36.2 us; N = 1536: 42.3 vs 43.2 us).
+inline bool multigroup_pays(int64_t n_tokens, bool glu) {
+  const int64_t tiles8 = (n_tokens + 7) / 8;
+  return tiles8 * 8 >= (int64_t)device_cu_count() * (glu ? 5 : 3);
+}
 void launch_forward_dmg(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt, void* y,
                         bool glu, hipStream_t s);
 bool dm64_eligible(int n_in, int b, int xdt, bool yf32);
@@ -605,9 +614,10 @@ void launch_dmk_image(int n_out, int n_in, void* spec, hipStream_t s);
 // fused BC-MLP (bcfft_dmm.hip): y = down(silu(gate(x)) * up(x)) in one launch; bf16 x and y,
 // b = 128, hidden 4096 (n_in = n_out = 32 blocks), intermediate n_h blocks with 32 < n_h <= 127
 bool dmm_eligible(int n_in, int b, int xdt, int n_h, int n_out);
-#ifndef BCFFT_DMM_MIN_TOKENS
-#define BCFFT_DMM_MIN_TOKENS 1       // the MLP's AUTO mode takes the fused kernel from this many tokens
-#endif
+// the MLP's AUTO mode takes the fused kernel once its 8-token tiles fill 3/8 of the CUs (N = 768 on
+// 256 CUs: 53.7 us vs 53.2 split; N = 1024: 57.7 vs 60.3; N = 256: 52.6 vs 34.0, the split form's
+// per-group gate/up kernel spreading over more CUs; profiles/r03h_dmg_switch.log)
+inline bool dmm_pays(int64_t n_tokens) { return multigroup_pays(n_tokens, false); }
 void launch_mlp_dmm(const void* x, int64_t n, int n_h, const void* spec_gu, const void* spec_dn, void* y,
                     hipStream_t s);
 

@@ -937,8 +937,8 @@ int bcfft_forward_glu(const void* x, int x_dtype, int64_t n_tokens, int in_featu
                                 BCFFT_ALGO_AUTO, stream);
 }
 
-// the fused BC-MLP's resolved mode: FUSED where bcfft_dmm.hip serves the geometry (AUTO: from
-// BCFFT_DMM_MIN_TOKENS tokens), else SPLIT; < 0 for invalid arguments
+// the fused BC-MLP's resolved mode: FUSED where bcfft_dmm.hip serves the geometry (AUTO: once its
+// tiles fill enough CUs, bcfft::dmm_pays), else SPLIT; < 0 for invalid arguments
 static int mlp_mode(int64_t n_tokens, int hidden_features, int inter_features, int block_size, int x_dtype, int mode) {
   if (mode != BCFFT_MLP_AUTO && mode != BCFFT_MLP_FUSED && mode != BCFFT_MLP_SPLIT) return -1;
   if (!valid_block(block_size) || !valid_dt(x_dtype) || n_tokens < 0 || hidden_features <= 0 || inter_features <= 0 ||
@@ -946,7 +946,7 @@ static int mlp_mode(int64_t n_tokens, int hidden_features, int inter_features, i
     return -1;
   const int n_hid = hidden_features / block_size, n_h = inter_features / block_size;
   const bool ok = bcfft::dmm_eligible(n_hid, block_size, x_dtype, n_h, n_hid);
-  if (mode == BCFFT_MLP_AUTO) return ok && n_tokens >= BCFFT_DMM_MIN_TOKENS ? BCFFT_MLP_FUSED : BCFFT_MLP_SPLIT;
+  if (mode == BCFFT_MLP_AUTO) return ok && bcfft::dmm_pays(n_tokens) ? BCFFT_MLP_FUSED : BCFFT_MLP_SPLIT;
   return mode;
 }
 

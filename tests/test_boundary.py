@@ -206,13 +206,15 @@ def test_mlp_mode_and_workspace_without_gpu(built_lib):
     AUTO, FUSED, SPLIT = (_lib.MLP_MODES[m] for m in ("auto", "fused", "split"))
     F32, BF16 = _lib.BCFFT_F32, _lib.BCFFT_BF16
     assert wb(8192, 4096, 11008, 128, BF16, AUTO) == 0
+    assert wb(768, 4096, 11008, 128, BF16, AUTO) == 0                  # 96 tiles = 3/8 of 256 CUs
+    assert wb(760, 4096, 11008, 128, BF16, AUTO) == 760 * 11008 * 2      # fewer: the split form
     assert wb(1, 4096, 11008, 128, BF16, FUSED) == 0
     assert wb(8192, 4096, 11008, 128, BF16, SPLIT) == 8192 * 11008 * 2
     assert wb(7, 4096, 11008, 128, F32, AUTO) == (7 * 11008 * 4 + 15) // 16 * 16   # fp32: split
     assert wb(5, 4096, 11008, 64, BF16, AUTO) == 5 * 11008 * 2                      # b = 64: split
     assert wb(5, 4096, 4096, 128, BF16, AUTO) == 5 * 4096 * 2                       # 32 h blocks: split
     assert wb(5, 4096, 16384, 128, BF16, AUTO) == 5 * 16384 * 2                     # 128 h blocks: split
-    assert wb(5, 4096, 16256, 128, BF16, AUTO) == 0                                 # 127 h blocks
+    assert wb(1024, 4096, 16256, 128, BF16, AUTO) == 0                              # 127 h blocks
     assert wb(5, 4096, 11008, 128, BF16, 3) == -1
     assert wb(5, 4000, 11008, 128, BF16, AUTO) == -1
     fake = 4096

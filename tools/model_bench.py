@@ -10,8 +10,8 @@ padded batches and model.generate. Here:
     tokenizer exist offline), and prompts are synthetic token ids with seeded lengths: the
     metrics show the harness working, not LLaMA quality;
   * patch_linear_with_block_circulant (q/k/v/o/gate/up/down; --targets mlp for the reference's
-    MLP-only patch), then fuse_attention_qkv and fuse_mlp_gate_up (one launch for q/k/v, one for
-    gate/up + SwiGLU);
+    MLP-only patch), then fuse_attention_qkv and fuse_mlp_gate_up (one launch for q/k/v; the
+    whole MLP in one launch when all its projections are BC, else one for gate/up + SwiGLU);
   * multi-GPU (config 5): one process per GPU under torch.distributed.run; each rank holds the
     whole model and takes a contiguous slice of the prompts (prompt-level replicas, no collective
     in the forward); at the end ONE all-gather (RCCL) of the last-token logits. Throughput is all
@@ -132,9 +132,12 @@ def projection_parity(model, layer_idx, batch):
             hooks.append(mod.register_forward_hook(_keep(seen, name, lambda m, inp, out: (m, inp[0], out))))
     # the fused gate/up launch bypasses gate_proj/up_proj's __call__: capture the MLP input and
     # down_proj's input (= silu(gate(x)) * up(x)) instead
+    # the one-launch MLP (bcfft_forward_mlp) bypasses all three projections: capture the MLP's
+    # input and output
     mlp_io = {}
     if hasattr(layer.mlp, "_bc_gate_up"):
         hooks.append(layer.mlp.register_forward_hook(_keep(mlp_io, "x", lambda m, inp, out: inp[0])))
+        hooks.append(layer.mlp.register_forward_hook(_keep(mlp_io, "y", lambda m, inp, out: out)))
         hooks.append(layer.mlp.down_proj.register_forward_pre_hook(_keep(mlp_io, "h", lambda m, inp: inp[0])))
     ids, mask, _ = batch
     try:
@@ -152,6 +155,18 @@ def projection_parity(model, layer_idx, batch):
                 "tokens": int(out.shape[0])}
 
     errs = {}
+    if "x" in mlp_io and "h" not in mlp_io:           # the whole MLP ran as one launch
+        g, u, d = layer.mlp.gate_proj, layer.mlp.up_proj, layer.mlp.down_proj
+        x = mlp_io["x"].reshape(-1, g.in_features)
+        y = mlp_io["y"].reshape(-1, d.out_features)
+        gr, ur = reference_bc_fp32(x, g.c, g.bias), reference_bc_fp32(x, u.c, u.bias)
+        ref = reference_bc_fp32(torch.nn.functional.silu(gr) * ur, d.c, d.bias)
+        errs["mlp(one launch)"] = score(y, ref)
+        # "rounded": torch's own bf16 sequence (gate, up, silu, product, down rounded to x dtype)
+        h_r = (torch.nn.functional.silu(gr.to(y.dtype)) * ur.to(y.dtype))
+        ref_r = reference_bc_fp32(h_r, d.c, d.bias).to(y.dtype).float()
+        errs["mlp(one launch)"].update(rel_err_vs_rounded=float((y.float() - ref_r).norm() / ref_r.norm()),
+                                       rounding_floor=float((ref_r - ref).norm() / ref.norm()))
     for name, (m, x, y) in seen.items():
         if name.endswith(("gate_proj", "up_proj")) and "h" in mlp_io:
             continue
