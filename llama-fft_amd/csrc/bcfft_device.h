@@ -571,12 +571,16 @@ bool dm8_eligible(int n_in, int b, int xdt, bool yf32);
 bool dmg_eligible(int n_in, int b, int xdt, bool yf32, int n_out, bool glu);
 // The multi-group kernels give one workgroup an 8-token tile for ALL its output groups, so a
 // launch has only ceil(N / 8) workgroups; the per-group kernels spread (tile, group) pairs over
-// the CUs. Measured at b = 128, bf16 (profiles/r03h_dmg_switch.log, 256 CUs): 4096 -> 11008 and
-// fused q/k/v pay from 96 tiles (N = 768: 18.2 vs 18.9 us; N = 20: 15.6 vs 9.7 us), the fused
-// gate/up + SwiGLU from ~160 tiles (N = 1024: 38.7 vs 36.2 us; N = 1536: 42.3 vs 43.2 us).
-inline bool multigroup_pays(int64_t n_tokens, bool glu) {
+// the CUs. They pay once the tiles fill `eighths` / 8 of the CUs. Measured at bf16 on 256 CUs
+// (profiles/r03h_dmg_switch.log, profiles/r03i_mg_switch.log; multi-group vs per-group):
+//   b = 128 4096 -> 11008 and q/k/v: 3/8 (N = 768: 18.2 vs 18.9 us; N = 20: 15.6 vs 9.7 us)
+//   b = 128 fused gate/up + SwiGLU:   5/8 (N = 1024: 38.7 vs 36.2 us; N = 1536: 42.3 vs 43.2 us)
+//   b = 64 4096 -> 11008:             4/8 (N = 768: 25.4 vs 23.7 us; N = 1024: 26.9 vs 28.7 us)
+//   b = 64 fused gate/up + SwiGLU:    5/8 (N = 1024: 48.1 vs 42.4 us; N = 1536: 50.0 vs 59.2 us)
+//   b = 256 4096 -> 11008:            3/8 (N = 512: 18.5 vs 12.2 us; N = 768: 19.2 vs 19.9 us)
+inline bool multigroup_pays(int64_t n_tokens, int eighths) {
   const int64_t tiles8 = (n_tokens + 7) / 8;
-  return tiles8 * 8 >= (int64_t)device_cu_count() * (glu ? 5 : 3);
+  return tiles8 * 8 >= (int64_t)device_cu_count() * eighths;
 }
 void launch_forward_dmg(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt, void* y,
                         bool glu, hipStream_t s);
@@ -617,7 +621,7 @@ bool dmm_eligible(int n_in, int b, int xdt, int n_h, int n_out);
 // the MLP's AUTO mode takes the fused kernel once its 8-token tiles fill 3/8 of the CUs (N = 768 on
 // 256 CUs: 53.7 us vs 53.2 split; N = 1024: 57.7 vs 60.3; N = 256: 52.6 vs 34.0, the split form's
 // per-group gate/up kernel spreading over more CUs; profiles/r03h_dmg_switch.log)
-inline bool dmm_pays(int64_t n_tokens) { return multigroup_pays(n_tokens, false); }
+inline bool dmm_pays(int64_t n_tokens) { return multigroup_pays(n_tokens, 3); }
 void launch_mlp_dmm(const void* x, int64_t n, int n_h, const void* spec_gu, const void* spec_dn, void* y,
                     hipStream_t s);
 

@@ -675,7 +675,7 @@ bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, bool exact, const vo
 #ifndef BCFFT_NO_DM8
   if (!exact && dm8_eligible(n_in, b, xdt, yf32)) {  // bf16 I/O: 8 tokens per tile
 #ifndef BCFFT_NO_DMG
-    if (dmg_eligible(n_in, b, xdt, yf32, n_out, false) && multigroup_pays(n, false)) {   // x transformed once (bcfft_dmg.hip)
+    if (dmg_eligible(n_in, b, xdt, yf32, n_out, false) && multigroup_pays(n, 3)) {   // x transformed once (bcfft_dmg.hip)
       launch_forward_dmg(x, n, n_out, spec, bias, bias_dt, y, false, s);
       return true;
     }
@@ -706,7 +706,7 @@ bool launch_forward_dm_glu(int b, int n_in, int xdt, bool exact, const void* x, 
     if (exact) launch_dm<BCFFT_BF16, false, true, true>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
 #ifndef BCFFT_NO_DM8
 #ifndef BCFFT_NO_DMG
-    else if (dmg_eligible(n_in, b, xdt, false, n_gate, true) && multigroup_pays(n, true))
+    else if (dmg_eligible(n_in, b, xdt, false, n_gate, true) && multigroup_pays(n, 5))
       launch_forward_dmg(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, true, s);   // x transformed once per tile
 #endif
     else launch_forward_dm8(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, true, s);   // 8 tokens per tile

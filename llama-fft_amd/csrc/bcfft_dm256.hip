@@ -1479,7 +1479,7 @@ void launch_forward_dm256(const void* x, int64_t n, int n_in, int n_out, const v
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
   const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
 #ifndef BCFFT_NO_DM256G
-  if (n_in == d256::NI && groups >= 3 && groups <= d256::MAXG) {   // several groups: x transformed once
+  if (n_in == d256::NI && groups >= 3 && groups <= d256::MAXG && multigroup_pays(n, 3)) {   // x transformed once
     const int64_t wgs = device_cu_count() < n_mtiles ? device_cu_count() : n_mtiles;
     hipLaunchKernelGGL(bc_forward_dm256g_kernel<false>, dim3((unsigned)wgs), dim3(512), 0, s, x, n, n_out, stat, osc,
                        bias, bias_dt, y);

@@ -427,7 +427,7 @@ bool dm64_eligible(int n_in, int b, int xdt, bool yf32) { return b == 64 && n_in
 void launch_forward_dm64(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt,
                          void* y, bool glu, hipStream_t s) {
 #ifndef BCFFT_NO_DM64G
-  if (dm64g_eligible(64, 64, BCFFT_BF16, false, n_out, glu)) {   // several groups: x transformed once
+  if (dm64g_eligible(64, 64, BCFFT_BF16, false, n_out, glu) && multigroup_pays(n, glu ? 5 : 4)) {   // x transformed once
     launch_forward_dm64g(x, n, n_out, spec, bias, bias_dt, y, glu, s);
     return;
   }
