@@ -578,9 +578,15 @@ bool dmg_eligible(int n_in, int b, int xdt, bool yf32, int n_out, bool glu);
 //   b = 64 4096 -> 11008:             4/8 (N = 768: 25.4 vs 23.7 us; N = 1024: 26.9 vs 28.7 us)
 //   b = 64 fused gate/up + SwiGLU:    5/8 (N = 1024: 48.1 vs 42.4 us; N = 1536: 50.0 vs 59.2 us)
 //   b = 256 4096 -> 11008:            3/8 (N = 512: 18.5 vs 12.2 us; N = 768: 19.2 vs 19.9 us)
+// Past one round of tiles a persistent multi-group launch takes ceil(tiles / CUs) whole tile
+// times, so it also needs the last round well filled: at least 3/4 of the CUs' share per round
+// (N = 2380, 298 tiles on 256 CUs: 2 rounds of 149 -> per-group; N = 3072: 2 rounds of 192 ->
+// level with per-group, 78.4 vs 76.9 us for the fused gate/up; N = 4096 and up: multi-group).
 inline bool multigroup_pays(int64_t n_tokens, int eighths) {
-  const int64_t tiles8 = (n_tokens + 7) / 8;
-  return tiles8 * 8 >= (int64_t)device_cu_count() * eighths;
+  const int64_t tiles8 = (n_tokens + 7) / 8, cus = device_cu_count();
+  if (tiles8 * 8 < cus * eighths) return false;
+  const int64_t rounds = (tiles8 + cus - 1) / cus;
+  return rounds == 1 || tiles8 * 4 >= rounds * cus * 3;
 }
 void launch_forward_dmg(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt, void* y,
                         bool glu, hipStream_t s);

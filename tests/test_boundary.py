@@ -208,6 +208,8 @@ def test_mlp_mode_and_workspace_without_gpu(built_lib):
     assert wb(8192, 4096, 11008, 128, BF16, AUTO) == 0
     assert wb(768, 4096, 11008, 128, BF16, AUTO) == 0                  # 96 tiles = 3/8 of 256 CUs
     assert wb(760, 4096, 11008, 128, BF16, AUTO) == 760 * 11008 * 2      # fewer: the split form
+    assert wb(2380, 4096, 11008, 128, BF16, AUTO) == 2380 * 11008 * 2    # 298 tiles: 2 thin rounds
+    assert wb(3072, 4096, 11008, 128, BF16, AUTO) == 0                   # 2 rounds of 192 tiles
     assert wb(1, 4096, 11008, 128, BF16, FUSED) == 0
     assert wb(8192, 4096, 11008, 128, BF16, SPLIT) == 8192 * 11008 * 2
     assert wb(7, 4096, 11008, 128, F32, AUTO) == (7 * 11008 * 4 + 15) // 16 * 16   # fp32: split

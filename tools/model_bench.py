@@ -155,17 +155,17 @@ def projection_parity(model, layer_idx, batch):
                 "tokens": int(out.shape[0])}
 
     errs = {}
-    if "x" in mlp_io and "h" not in mlp_io:           # the whole MLP ran as one launch
+    if "x" in mlp_io and "h" not in mlp_io:           # the whole MLP ran through bcfft_forward_mlp
         g, u, d = layer.mlp.gate_proj, layer.mlp.up_proj, layer.mlp.down_proj
         x = mlp_io["x"].reshape(-1, g.in_features)
         y = mlp_io["y"].reshape(-1, d.out_features)
         gr, ur = reference_bc_fp32(x, g.c, g.bias), reference_bc_fp32(x, u.c, u.bias)
         ref = reference_bc_fp32(torch.nn.functional.silu(gr) * ur, d.c, d.bias)
-        errs["mlp(one launch)"] = score(y, ref)
+        errs["mlp(bcfft_forward_mlp)"] = score(y, ref)
         # "rounded": torch's own bf16 sequence (gate, up, silu, product, down rounded to x dtype)
         h_r = (torch.nn.functional.silu(gr.to(y.dtype)) * ur.to(y.dtype))
         ref_r = reference_bc_fp32(h_r, d.c, d.bias).to(y.dtype).float()
-        errs["mlp(one launch)"].update(rel_err_vs_rounded=float((y.float() - ref_r).norm() / ref_r.norm()),
+        errs["mlp(bcfft_forward_mlp)"].update(rel_err_vs_rounded=float((y.float() - ref_r).norm() / ref_r.norm()),
                                        rounding_floor=float((ref_r - ref).norm() / ref.norm()))
     for name, (m, x, y) in seen.items():
         if name.endswith(("gate_proj", "up_proj")) and "h" in mlp_io:
