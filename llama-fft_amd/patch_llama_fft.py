@@ -20,6 +20,7 @@ What differs, by design:
 """
 from __future__ import annotations
 
+import functools
 import os
 from typing import Dict
 
@@ -239,58 +240,59 @@ class BlockCirculantLinear(nn.Module):
 
 # ----------------------------------------------------------------------------- param I/O
 def _get_submodule_by_name(model: nn.Module, name: str) -> nn.Module:
-    """patch_llama_fft.py:278-284."""
-    cur = model
-    if name == "":
-        return cur
-    for part in name.split("."):
-        cur = getattr(cur, part)
-    return cur
+    """patch_llama_fft.py:278-284: the attribute path `name` ("" = the model itself);
+    AttributeError for a missing step."""
+    return functools.reduce(getattr, name.split("."), model) if name else model
+
+
+def _bc_tensors(model: nn.Module):
+    """(checkpoint key, tensor) of every BlockCirculantLinear's c and bias, in module order."""
+    for prefix, mod in model.named_modules():
+        if isinstance(mod, BlockCirculantLinear):
+            yield f"{prefix}.c", mod.c
+            if mod.bias is not None:
+                yield f"{prefix}.bias", mod.bias
 
 
 def save_bc_params(model: nn.Module, path: str) -> None:
-    """patch_llama_fft.py:287-300 — {"<module>.c": (nO,nI,b), "<module>.bias": (M,)} via torch.save."""
-    bc_state: Dict[str, torch.Tensor] = {}
-    for module_name, module in model.named_modules():
-        if isinstance(module, BlockCirculantLinear):
-            bc_state[f"{module_name}.c"] = module.c.detach().cpu()
-            if module.bias is not None:
-                bc_state[f"{module_name}.bias"] = module.bias.detach().cpu()
-    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
-    torch.save(bc_state, path)
-    print(f"Saved BC params: {len(bc_state)} tensors -> {path}")
+    """patch_llama_fft.py:287-300: torch.save of {"<module>.c": (nO,nI,b), "<module>.bias": (M,)}
+    for every BC module, host copies."""
+    state = {key: t.detach().cpu() for key, t in _bc_tensors(model)}
+    parent = os.path.dirname(path)
+    os.makedirs(parent if parent else ".", exist_ok=True)
+    torch.save(state, path)
+    print(f"Saved BC params: {len(state)} tensors -> {path}")
+
+
+def _load_target(model: nn.Module, key: str, value: torch.Tensor, strict_shapes: bool):
+    """The parameter a checkpoint entry restores, or None when the reference loader skips it
+    (patch_llama_fft.py:311-336): not a .c / .bias key, no such module or attribute, not a
+    tensor, or (strict_shapes) a shape mismatch."""
+    if not key.endswith((".c", ".bias")):
+        return None
+    owner_name, attr = key.rsplit(".", 1)
+    try:
+        owner = _get_submodule_by_name(model, owner_name)
+    except AttributeError:
+        return None
+    target = getattr(owner, attr, None)
+    if not isinstance(target, torch.Tensor) or (strict_shapes and target.shape != value.shape):
+        return None
+    return target
 
 
 def load_bc_params(model: nn.Module, path: str, *, strict_shapes: bool = True) -> None:
-    """patch_llama_fft.py:303-340 — load a save_bc_params checkpoint (tensors only:
-    weights_only=True), skipping unknown names and mismatched shapes."""
+    """patch_llama_fft.py:303-340: restore a save_bc_params checkpoint in place (tensors only,
+    torch.load(weights_only=True)); entries without a matching parameter are counted as skipped."""
     state: Dict[str, torch.Tensor] = torch.load(path, map_location="cpu", weights_only=True)
-    loaded = 0
-    skipped = 0
-    for full_name, tensor in state.items():
-        if not (full_name.endswith(".c") or full_name.endswith(".bias")):
-            skipped += 1
-            continue
-        module_name, param_name = full_name.rsplit(".", 1)
-        try:
-            module = _get_submodule_by_name(model, module_name)
-        except AttributeError:
-            skipped += 1
-            continue
-        if not hasattr(module, param_name):
-            skipped += 1
-            continue
-        param = getattr(module, param_name)
-        if not isinstance(param, torch.Tensor):
-            skipped += 1
-            continue
-        if strict_shapes and param.shape != tensor.shape:
-            skipped += 1
-            continue
-        with torch.no_grad():
-            param.copy_(tensor.to(param.device, dtype=param.dtype))
-        loaded += 1
-    print(f"Loaded BC params from {path}: loaded={loaded}, skipped={skipped}")
+    restored = 0
+    with torch.no_grad():
+        for key, value in state.items():
+            target = _load_target(model, key, value, strict_shapes)
+            if target is not None:
+                target.copy_(value.to(target.device, dtype=target.dtype))
+                restored += 1
+    print(f"Loaded BC params from {path}: loaded={restored}, skipped={len(state) - restored}")
 
 
 # ----------------------------------------------------------------------------- model patcher

@@ -84,6 +84,26 @@ def test_save_load_roundtrip(plf, tmp_path):
     assert not torch.equal(net3[0].c.flatten()[:10], net[0].c.flatten()[:10])
 
 
+def test_load_skips_like_the_reference(plf, tmp_path, capsys):
+    """load_bc_params (patch_llama_fft.py:303-340): entries that are not .c / .bias, name no
+    module or attribute, or mismatch in shape are skipped and counted; the rest are copied in
+    the parameter's dtype."""
+    net = torch.nn.Sequential(plf.BlockCirculantLinear(128, 128, block_size=64))
+    p = os.path.join(tmp_path, "bc.pt")
+    state = {"0.c": torch.randn(2, 2, 64, dtype=torch.float64), "0.bias": torch.randn(128),
+             "0.weight": torch.randn(3), "7.c": torch.randn(2, 2, 64), "0.zz.c": torch.randn(1),
+             "0.c.bias": torch.randn(1)}
+    torch.save(state, p)
+    plf.load_bc_params(net, p)
+    out = capsys.readouterr().out
+    assert "loaded=2, skipped=4" in out, out
+    assert net[0].c.dtype == torch.float32 and torch.equal(net[0].c, state["0.c"].float())
+    assert torch.equal(net[0].bias, state["0.bias"])
+    torch.save({"0.c": torch.randn(1, 2, 64)}, p)
+    plf.load_bc_params(net, p, strict_shapes=False)       # non-strict: copy_ broadcasts or raises
+    assert "loaded=1, skipped=0" in capsys.readouterr().out
+
+
 def _tiny_llama():
     from transformers import LlamaConfig, LlamaForCausalLM
     cfg = LlamaConfig(vocab_size=64, hidden_size=256, intermediate_size=512, num_hidden_layers=3,
