@@ -133,6 +133,14 @@ def mlp_fused_eligible(hidden_features: int, inter_features: int, block_size: in
             and 32 < inter_features // 128 <= 127 and dtype in (None, torch.bfloat16))
 
 
+def mlp_auto_is_fused(n_tokens: int, hidden_features: int, inter_features: int, block_size: int,
+                      dtype: torch.dtype) -> bool:
+    """Whether bcfft_forward_mlp's AUTO mode runs the one-launch kernel for these sizes (it needs
+    no workspace exactly then)."""
+    return _lib.load().bcfft_forward_mlp_workspace_bytes(n_tokens, hidden_features, inter_features, block_size,
+                                                         _lib.dtype_code(dtype), _lib.MLP_MODES["auto"]) == 0
+
+
 def glu_eligible(in_features: int, block_size: int, dtype: torch.dtype | None = None) -> bool:
     """Geometries the fused gate/up kernel serves (include/bcfft.h): the stationary ones, and
     b = 256 with K = 4096 for bf16 x (the b = 256 multi-group DFT kernel)."""
@@ -152,13 +160,14 @@ def default_algo() -> str:
 
 
 def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, block_size: int,
-            out_features: int, algo: str | None = None) -> torch.Tensor:
+            out_features: int, algo: str | None = None, split_k: bool = True) -> torch.Tensor:
     """y = BC(x2d) (+ bias) with one fused kernel. x2d: (N, K) device tensor.
     algo: "auto" (at b = 128, K = 4096: dftx for fp32 outputs, dft for 16-bit ones; dft on its
     other geometries; else stationary where eligible, else mfma for b <= 128, else valu), "dft" (block DFTs and MAC on fp16 MFMA, weights in VGPRs, ~3.5e-4), "dftx"
     (dft with the per-bin products split hi + lo: ~2.8e-4, linear to ~1e-6),
     "stationary" (weights in VGPRs, fp16 MFMA, ~3e-4), "mfma" (split-bf16, ~1e-5) or
-    "valu" (exact fp32 MAC). See include/bcfft.h."""
+    "valu" (exact fp32 MAC). See include/bcfft.h. split_k=False withholds the workspace, so short
+    grids run unsplit (the split-K forms sum fp32 partials: not bit-identical to the unsplit launch)."""
     _lib.require_device(x2d, "bcfft.forward")
     n, k = x2d.shape
     if block_size > 0 and out_features % block_size == 0 and k % block_size == 0:
@@ -178,9 +187,12 @@ def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, bl
         bias_ptr, bias_code = bias.data_ptr(), _lib.dtype_code(bias.dtype)
     lib = _lib.load()
     code = _lib.ALGOS[(algo or default_algo()).lower()]
-    # split-K workspace (short grids of the MFMA kernel); caller-owned, from torch's allocator
+    # split-K workspace (short grids of the MFMA and streamed-weight kernels); caller-owned, from
+    # torch's allocator
     ws_bytes = lib.bcfft_forward_workspace_bytes_io(n, k, out_features, block_size, code,
                                                     _lib.dtype_code(x2d.dtype), _lib.dtype_code(out_dtype))
+    if not split_k:
+        ws_bytes = 0
     ws = torch.empty(max(ws_bytes, 0), dtype=torch.uint8, device=x2d.device) if ws_bytes > 0 else None
     _lib.check(lib.bcfft_forward_ws(x2d.data_ptr(), _lib.dtype_code(x2d.dtype), n, k, out_features,
                                     block_size, spec.data_ptr(), bias_ptr, bias_code, y.data_ptr(),

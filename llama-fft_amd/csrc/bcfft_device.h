@@ -621,6 +621,11 @@ bool dmk_eligible(int n_in, int b, int xdt, bool yf32);
 void launch_forward_dmk(const void* x, int64_t n, int n_in, int n_out, const void* spec, const void* bias,
                         int bias_dt, void* y, hipStream_t s);
 void launch_dmk_image(int n_out, int n_in, void* spec, hipStream_t s);
+// its K-chunk split for short grids (decode sizes): kz slices write fp32 partials to a caller
+// workspace of kz x n x n_out * 128 floats, a finishing pass sums them; dmk_ksplit: 1 = no split
+int dmk_ksplit(int64_t n, int n_in, int n_out);
+void launch_forward_dmk_split(const void* x, int64_t n, int n_in, int n_out, const void* spec, const void* bias,
+                              int bias_dt, void* y, float* ws, int kz, hipStream_t s);
 // fused BC-MLP (bcfft_dmm.hip): y = down(silu(gate(x)) * up(x)) in one launch; bf16 x and y,
 // b = 128, hidden 4096 (n_in = n_out = 32 blocks), intermediate n_h blocks with 32 < n_h <= 127
 bool dmm_eligible(int n_in, int b, int xdt, int n_h, int n_out);

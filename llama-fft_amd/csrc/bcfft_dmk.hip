@@ -37,6 +37,7 @@
 #include "bcfft_device.h"
 #include "bcfft_dm_table.h"
 #include "bcfft_dm_common.h"
+#include <algorithm>
 
 namespace bcfft {
 
@@ -82,10 +83,14 @@ __device__ __forceinline__ uint32_t f16_pow2_neg(int d) {
 }
 }  // namespace dmk
 
-template <int TT>
+// SPL (decode / short-prefill sizes, bc_dmk_finish_kernel): the K-chunks are split into kz slices;
+// workgroup b takes slice b % kz of exactly one (group, tile) and writes its partial y in fp32 to
+// ws[slice][token][column] (no rounding, no bias), and a finishing pass sums the slices.
+template <int TT, bool SPL = false>
 __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_in, int n_out, const uint32_t* __restrict__ stat,
-    const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
+    const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv,
+    int kz, float* __restrict__ ws) {
   using namespace dmk;
   using G = Geo<TT>;
   constexpr int MT = G::MT, TPW = G::TPW, NDMA = G::NDMA, REGION = G::REGION, F_OFF = G::F_OFF;
@@ -99,13 +104,27 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n_groups = (n_out + NOG - 1) / NOG;
-  const GroupMap gm = group_map(n_groups);          // XCD-aware when the grid allows it
-  const int grp_o = gm.grp, wg_in_grp = gm.lane;
   const int64_t K = (int64_t)n_in * B;
   const int64_t M = (int64_t)n_out * B;
   const int nch = (n_in + 15) / 16;
   const int64_t n_mtiles = (n_tokens + TT - 1) / TT;
-  const int gstride = gm.stride;
+  // chunk range [c0, c1) of this workgroup; unsplit: all chunks, persistent over tiles
+  int grp_o, wg_in_grp, gstride, c0 = 0, c1 = nch, slice = 0;
+  if constexpr (SPL) {                              // grid = kz x groups x tiles, one tile each
+    slice = blockIdx.x % kz;
+    const int rest = blockIdx.x / kz;
+    grp_o = rest % n_groups;
+    wg_in_grp = rest / n_groups;
+    gstride = (int)n_mtiles;
+    const int cps = (nch + kz - 1) / kz;
+    c0 = slice * cps;
+    c1 = min(nch, c0 + cps);
+  } else {
+    const GroupMap gm = group_map(n_groups);        // XCD-aware when the grid allows it
+    grp_o = gm.grp;
+    wg_in_grp = gm.lane;
+    gstride = gm.stride;
+  }
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
   const uint4* bimg = reinterpret_cast<const uint4*>(stat + 4);
 #ifdef BCFFT_STAMPS
@@ -411,6 +430,11 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
   // stored as 1 KiB buffer stores; bcfft_dm8.hip's stage 3. tok < 0: nothing is stored.
   auto stage3 = [&](char* region, int tl, int rref, int64_t tok) {
     if constexpr ((ABL & 8) != 0) return;
+    // SPL: a real token's partial y goes to ws in fp32 straight from registers (4 consecutive
+    // columns per lane and store); tok < 0 keeps the staged path (8 dropped stores), whose count
+    // the first stage 2's hand-counted wait relies on
+    const bool part = SPL && tok >= 0;
+    float* wsp = SPL ? ws + ((int64_t)slice * n_tokens + (tok >= 0 ? tok : 0)) * M + (int64_t)grp_o * NOG * B : nullptr;
     const int l = opaque(lane);
     const int o16 = l & 15, g = l >> 4;
     char* slot = region + tl * YSLOT;
@@ -473,6 +497,11 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = hf ? fmaf(E[nt][r], ysc[nt], -os[r]) : fmaf(E[nt][r], ysc[nt], os[r]);
+          if (part) {
+            if (tok_ok && o < nvalid)
+              *reinterpret_cast<float4*>(wsp + o * B + 16 * mt + 4 * g + 64 * hf) = make_float4(v[0], v[1], v[2], v[3]);
+            continue;
+          }
           if (bias_dt != BCFFT_NONE) {              // .to(x dtype) :266, + bias :270-271
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = round_to(v[r], XT);
@@ -493,6 +522,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
           for (int pr = 0; pr < 2; ++pr) gcur[ks][pr] = gnxt[ks][pr];
       }
     }
+    if (part) return;
     constexpr int RB = B * ESY;
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
         (char*)yv + (tok_ok ? tok : 0) * M * ESY + (int64_t)grp_o * NOG * RB, 0,
@@ -516,7 +546,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
 
   // ---- prologue: the first tile's chunk 0, the DFT table
   u32x4 breg[BPW][NT];
-  dma_chunk(wg_in_grp, 0, lds);
+  dma_chunk(wg_in_grp, c0, lds);
   {
     const uint4* tab = reinterpret_cast<const uint4*>(kDmF);
 #pragma unroll
@@ -556,8 +586,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
       char* region = lds + rsel * REGION;
       char* other = lds + (rsel ^ 1) * REGION;
       DSTAMP(0);
-      load_b(0, 0, breg);                           // B(0): issued here, not carried across the
-      load_b(0, 1, breg);                           // tile end (the accumulators are dead now)
+      load_b(c0, 0, breg);                          // B(c0): issued here, not carried across the
+      load_b(c0, 1, breg);                          // tile end (the accumulators are dead now)
       wait_vmcnt<16 + 8 * (MT - 1)>();              // x(0): older than B(0) and a half tile's stores
       // stage 1 of this tile and the deferred stage 3 of the previous one touch different
       // regions: one barrier for both, and the scheduler may interleave them
@@ -567,25 +597,26 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
       DSTAMP(3);
       lds_barrier();                                // B0 + Ba: X(0) complete, the other region free
       DSTAMP(4);
-      dma_chunk(m, 1, other);
-      stage2(region, breg, 1, std::true_type{});
+      if (c0 + 1 < c1) dma_chunk(m, c0 + 1, other);
+      else dma_chunk(m + gstride, c0, other);       // one chunk: the next tile's first (or nothing)
+      stage2(region, breg, c0 + 1 < c1 ? c0 + 1 : -1, std::true_type{});
       DSTAMP(5);
       lds_barrier();                                // Bb
       DSTAMP(6);
       rsel ^= 1;
     }
     // ---- steps 1 .. nch - 1
-    for (int c = 1; c < nch; ++c) {
+    for (int c = c0 + 1; c < c1; ++c) {
       char* region = lds + rsel * REGION;
       char* other = lds + (rsel ^ 1) * REGION;
       wait_vmcnt<16>();                             // x(c) (older than B(c))
-      if (c + 1 < nch) dma_chunk(m, c + 1, other);
-      else dma_chunk(m + gstride, 0, other);        // zero-filled past the last tile
+      if (c + 1 < c1) dma_chunk(m, c + 1, other);
+      else dma_chunk(m + gstride, c0, other);       // zero-filled past the last tile
       stage1(region);
       if (c <= 5) DSTAMP(7 + 3 * (c - 1));
       lds_barrier();                                // Ba
       if (c <= 5) DSTAMP(8 + 3 * (c - 1));
-      stage2(region, breg, c + 1 < nch ? c + 1 : -1, std::false_type{});
+      stage2(region, breg, c + 1 < c1 ? c + 1 : -1, std::false_type{});
       lds_barrier();                                // Bb
       if (c <= 5) DSTAMP(9 + 3 * (c - 1));
       rsel ^= 1;
@@ -679,11 +710,64 @@ void launch_forward_dmk(const void* x, int64_t n, int n_in, int n_out, const voi
   const int64_t n_mtiles = t16 ? (n + 15) / 16 : (n + 7) / 8;
   const int64_t total = group_grid(cus, groups, n_mtiles);
   if (t16)
-    hipLaunchKernelGGL(bc_forward_dmk_kernel<16>, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat,
-                       osc, bias, bias_dt, y);
+    hipLaunchKernelGGL((bc_forward_dmk_kernel<16, false>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out,
+                       stat, osc, bias, bias_dt, y, 1, nullptr);
   else
-    hipLaunchKernelGGL(bc_forward_dmk_kernel<8>, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat,
-                       osc, bias, bias_dt, y);
+    hipLaunchKernelGGL((bc_forward_dmk_kernel<8, false>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out,
+                       stat, osc, bias, bias_dt, y, 1, nullptr);
+}
+
+// the split form's finishing pass: y = (sum over the kz slices in order, rounded to bf16) + bias,
+// rounded (the unsplit kernel's epilogue: .to(x dtype) :266, + bias :270-271); 4 columns a thread
+__global__ void bc_dmk_finish_kernel(const float* __restrict__ ws, int kz, int64_t n_tokens, int64_t M,
+                                     const void* __restrict__ bias, int bias_dt, uint16_t* __restrict__ y) {
+  const int64_t quads = n_tokens * M / 4;
+  const int64_t slab = n_tokens * M;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < quads; q += (int64_t)gridDim.x * blockDim.x) {
+    float4 a = reinterpret_cast<const float4*>(ws)[q];
+    for (int z = 1; z < kz; ++z) {
+      const float4 b = reinterpret_cast<const float4*>(ws + z * slab)[q];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    float v[4] = {a.x, a.y, a.z, a.w};
+    if (bias_dt != BCFFT_NONE) {
+      const int64_t col = (q * 4) % M;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = round_to(v[r], BCFFT_BF16) + load_scalar(bias, col + r, bias_dt);
+    }
+    reinterpret_cast<uint2*>(y)[q] = make_uint2(pack16<BCFFT_BF16>(v[0], v[1]), pack16<BCFFT_BF16>(v[2], v[3]));
+  }
+}
+
+// K-chunk slices of the split form: only where the unsplit grid leaves almost every CU idle (at
+// most 1/16 of the CUs' worth of (group, 8-token tile) pairs), as many slices as fill the CUs,
+// >= 1 chunk each. Measured at 11008 -> 4096 (profiles/r03l_dmk_split.log, 256 CUs): N = 1 11.9 vs
+// 20.9 us unsplit, N = 20 15.2 vs 21.1, N = 128 20.2 vs 21.4; N = 256 24.6 vs 21.7 (the fp32
+// partials and the finishing pass grow with N)
+int dmk_ksplit(int64_t n, int n_in, int n_out) {
+  const int64_t units = (n + 7) / 8 * ((n_out + dmk::NOG - 1) / dmk::NOG);
+  const int64_t cus = device_cu_count();
+  const int nch = (n_in + 15) / 16;
+  if (n <= 0 || units * 16 > cus) return 1;
+  int kz = (int)std::min<int64_t>(nch, cus / units);
+  if (kz < 2) return 1;
+  const int cps = (nch + kz - 1) / kz;
+  return (nch + cps - 1) / cps;                     // every slice non-empty
+}
+
+void launch_forward_dmk_split(const void* x, int64_t n, int n_in, int n_out, const void* spec, const void* bias,
+                              int bias_dt, void* y, float* ws, int kz, hipStream_t s) {
+  const int groups = (n_out + dmk::NOG - 1) / dmk::NOG;
+  const SpecLayout sl = spec_layout(n_out, n_in, 128);
+  const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
+  const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
+  const int64_t total = (int64_t)kz * groups * ((n + 7) / 8);
+  hipLaunchKernelGGL((bc_forward_dmk_kernel<8, true>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat,
+                     osc, nullptr, BCFFT_NONE, y, kz, ws);
+  const int64_t M = (int64_t)n_out * 128;
+  const int64_t quads = n * M / 4;
+  const unsigned blocks = (unsigned)((quads + 255) / 256 < 4096 ? (quads + 255) / 256 : 4096);
+  hipLaunchKernelGGL(bc_dmk_finish_kernel, dim3(blocks), dim3(256), 0, s, ws, kz, n, M, bias, bias_dt, (uint16_t*)y);
 }
 
 void launch_dmk_image(int n_out, int n_in, void* spec, hipStream_t s) {

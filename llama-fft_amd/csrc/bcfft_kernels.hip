@@ -787,7 +787,12 @@ static int64_t ws_bytes_for(int64_t n_tokens, int in_features, int out_features,
     return -1;
   const int n_in = in_features / block_size;
   const int a = resolve_algo(algo, n_in, block_size, xdt, yf32, n_tokens);
-  // the DFT engines never take a workspace (the down projection's streamed-weight kernel included)
+  // the DFT engines take no workspace, except the down projection's streamed-weight kernel at
+  // short grids (its K-chunk split: kz fp32 partial slabs)
+  if (a == BCFFT_ALGO_DFT && bcfft::dmk_eligible(in_features / block_size, block_size, xdt, yf32)) {
+    const int kz = bcfft::dmk_ksplit(n_tokens, in_features / block_size, out_features / block_size);
+    return kz < 2 ? 0 : kz * n_tokens * (int64_t)out_features * (int64_t)sizeof(float);
+  }
   if (a == BCFFT_ALGO_DFT || a == BCFFT_ALGO_DFTX || a == BCFFT_ALGO_STAT) return 0;
   int kz = 1;
   if (a == BCFFT_ALGO_MFMA && block_size <= BCFFT_MFMA_MAXB) kz = mfma_ksplit(n_tokens, n_in, block_size);
@@ -846,7 +851,9 @@ int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_featur
   float* ws = (workspace && need > 0 && workspace_bytes >= need) ? (float*)workspace : nullptr;
   hipStream_t s = (hipStream_t)stream;
   if (algo == BCFFT_ALGO_DFT && dmk) {
-    bcfft::launch_forward_dmk(x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, s);
+    if (ws) bcfft::launch_forward_dmk_split(x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, ws,
+                                            bcfft::dmk_ksplit(n_tokens, n_in, n_out), s);
+    else bcfft::launch_forward_dmk(x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, s);
     return record_launch();
   }
   if (algo == BCFFT_ALGO_DFT && dm256) {

@@ -411,7 +411,11 @@ def _mlp_fused_ok(mlp, x: torch.Tensor) -> bool:
 
 
 def _fused_mlp_forward(self, x):
-    if _mlp_fused_ok(self, x):
+    # the one-launch kernel where bcfft_forward_mlp's AUTO takes it (its tiles fill the CUs);
+    # otherwise the gate/up launch and down_proj's own forward (which splits K at short grids)
+    if _mlp_fused_ok(self, x) and _ops.mlp_auto_is_fused(x.numel() // x.shape[-1], self.down_proj.out_features,
+                                                         self.down_proj.in_features, self.down_proj.block_size,
+                                                         x.dtype):
         gu, d = self._bc_gate_up, self.down_proj
         shape = x.shape
         x2d = gu._gate._flatten(x)

@@ -170,7 +170,9 @@ def test_forward_workspace_bytes_io_follows_the_engine(built_lib):
     wio = lib.bcfft_forward_workspace_bytes_io
     AUTO, MFMA = _lib.ALGOS["auto"], _lib.ALGOS["mfma"]
     F32, BF16 = _lib.BCFFT_F32, _lib.BCFFT_BF16
-    assert wio(100, 11008, 4096, 128, AUTO, BF16, BF16) == 0
+    assert wio(100, 11008, 4096, 128, AUTO, BF16, BF16) == 6 * 100 * 4096 * 4   # dmk K-chunk split: 6 slices
+    assert wio(128, 11008, 4096, 128, AUTO, BF16, BF16) == 6 * 128 * 4096 * 4    # 16 tiles: still split
+    assert wio(136, 11008, 4096, 128, AUTO, BF16, BF16) == 0                    # 17 tiles: unsplit
     assert wio(100, 11008, 4096, 128, AUTO, F32, F32) == 6 * 100 * 4096 * 4
     assert wio(100, 11008, 4096, 128, AUTO, BF16, F32) == 6 * 100 * 4096 * 4   # fp32 bias: not dmk
     assert wio(100, 11008, 4096, 128, MFMA, BF16, BF16) == 6 * 100 * 4096 * 4  # forced MFMA splits

@@ -130,10 +130,47 @@ def test_dmk_bf16_matches_numpy_model(dev):
     x[3, 2048:4096] *= 10.0
     x[9] *= 1e-4
     xr = O.round_to(x, O.BF16)
-    y, ref = _run(dev, x, c, None, "bfloat16", "bfloat16", algo="dft")
+    _, ref = _run(dev, x, c, None, "bfloat16", "bfloat16", algo="dft")
+    from bcfft import ops
+    spec = ops.spectra(torch.from_numpy(c).to(dev).to(torch.bfloat16))
+    y = ops.forward(torch.from_numpy(x).to(dev).to(torch.bfloat16), spec, None, b, m, algo="dft",
+                    split_k=False)                  # the unsplit kernel the model mirrors
     g = y.float().cpu().numpy()
     mdl = O.round_to(dm_forward(xr, O.round_to(c, O.BF16), head=4), O.BF16)
     assert np.mean(g == mdl) > 0.97, np.mean(g == mdl)
     assert rel_err(g, mdl) < 1e-3
     for t in range(x.shape[0]):
         assert rel_err(g[t], ref[t]) < 4e-3, t
+
+
+@pytest.mark.parametrize("k,m,n,bias", [(11008, 4096, 1, False), (11008, 4096, 20, True), (11008, 4096, 37, False),
+                                        (11008, 4096, 128, True), (16256, 512, 9, False), (5120, 1024, 17, True)])
+def test_dmk_split_k_short_grids(dev, k, m, n, bias):
+    """Decode / short-prefill sizes: the K-chunks split over kz workgroup slices whose fp32 partial
+    outputs a finishing pass sums in a fixed order, then rounds (+ bias) once. Against the oracle
+    (bf16 bounds) and the unsplit launch (same numerics up to the partials' fp16 Y roundings)."""
+    from bcfft import _lib, ops
+    b = 128
+    lib = _lib.load()
+    wsb = lib.bcfft_forward_workspace_bytes_io(n, k, m, b, _lib.ALGOS["auto"], _lib.BCFFT_BF16, _lib.BCFFT_BF16)
+    assert wsb > 0 and wsb % (n * m * 4) == 0 and wsb // (n * m * 4) >= 2
+    rng = np.random.default_rng(k + 3 * n)
+    c = (rng.standard_normal((m // b, k // b, b)) * 0.01).astype(np.float32)
+    bv = (rng.standard_normal(m) * 0.1).astype(np.float32) if bias else None
+    x = rng.standard_normal((n, k)).astype(np.float32)
+    if n >= 11:
+        x[:11] = _extremes(rng, k)[:, :k] if k >= 11008 else x[:11]
+    y, ref = _run(dev, x, c, bv, "bfloat16", "bfloat16", algo="dft")
+    g = y.float().cpu().numpy()
+    for t in range(n):
+        if np.any(ref[t] != 0):
+            assert rel_err(g[t], ref[t]) < 4e-3, (t, rel_err(g[t], ref[t]))
+    spec = ops.spectra(torch.from_numpy(c).to(dev).to(torch.bfloat16))
+    bt = torch.from_numpy(bv).to(dev).to(torch.bfloat16) if bias else None
+    xt = torch.from_numpy(x).to(dev).to(torch.bfloat16)
+    yu = ops.forward(xt, spec, bt, b, m, algo="dft", split_k=False)
+    d = (y.float() - yu.float()).abs()
+    rms = yu.float().pow(2).mean().sqrt().item()
+    assert (d <= 2.0 ** -7 * (yu.float().abs() + rms)).float().mean().item() > 0.999
+    assert ((y.float() - yu.float()).norm() / yu.float().norm()).item() < 3e-3
+    assert torch.equal(y, ops.forward(xt, spec, bt, b, m, algo="dft"))     # deterministic

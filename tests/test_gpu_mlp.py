@@ -168,15 +168,22 @@ def test_llama_mlp_module_runs_one_launch(dev):
     P.patch_linear_with_block_circulant(model, num_layers_to_patch=1, block_size=128)   # c stays fp32
     ids = torch.randint(0, 256, (2, 16), device=dev)
     mlp = model.model.layers[0].mlp
-    x = torch.randn(2, 16, 4096, device=dev).to(torch.bfloat16)
+    x = torch.randn(2, 512, 4096, device=dev).to(torch.bfloat16)     # 1024 tokens: AUTO is fused
+    xs = x[:, :16]                                                    # 32 tokens: the two launches
+    from bcfft import ops
     with torch.no_grad():
         ref = model(input_ids=ids).logits.float()
         assert P.fuse_mlp_gate_up(model) == 1
-        assert P._mlp_fused_ok(mlp, x)
+        assert P._mlp_fused_ok(mlp, x) and ops.mlp_auto_is_fused(1024, 4096, 11008, 128, torch.bfloat16)
+        assert not ops.mlp_auto_is_fused(32, 4096, 11008, 128, torch.bfloat16)
         y1 = mlp(x)
-        y2 = mlp.down_proj(mlp._bc_gate_up(x))
+        sgu, sd = mlp._bc_gate_up._spectra(), mlp.down_proj._spectra(mlp.down_proj.c)
+        y2 = ops.forward_mlp(x.reshape(-1, 4096), sgu, sd, 128, 11008, mode="split").view_as(y1)
+        ys = mlp(xs)
+        ys2 = ops.forward_mlp(xs.reshape(-1, 4096), sgu, sd, 128, 11008, mode="split").view_as(ys)
         out = model(input_ids=ids).logits.float()
-    assert torch.equal(y1, y2)
+    assert torch.equal(y1, y2)                      # one launch == the two-launch form, bit for bit
+    assert ((ys.float() - ys2.float()).norm() / ys2.float().norm()).item() < 3e-3   # split-K down
     assert ((out - ref).norm() / ref.norm()).item() < 2e-2
 
 
