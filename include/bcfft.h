@@ -130,7 +130,11 @@ int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_feat
 int64_t bcfft_forward_workspace_bytes(int64_t n_tokens, int in_features, int out_features, int block_size,
                                       int algo);
 
-/* The same for known I/O dtypes (y_dtype = promote(x_dtype, bias_dtype)): AUTO then resolves
+/* The same for known I/O dtypes (y_dtype = promote(x_dtype, bias_dtype)). Besides the MFMA / VALU
+ * splits above, this also sizes the K-chunk split of the bf16 streamed-weight DFT kernel (b = 128,
+ * K > 4096: the down projection) at decode sizes (at most 1/16 of the CUs' worth of 8-token tiles
+ * x output groups): up to 6 slices of its 16-block K-chunks write fp32 partials (kz x n_tokens x
+ * out_features floats) that a finishing pass sums in order, rounds and biases. AUTO then resolves
  * exactly as bcfft_forward_ws will, so geometries that run a DFT engine for these dtypes (e.g. the
  * bf16 down projection on the streamed-weight kernel) report 0. < 0 for invalid arguments. */
 int64_t bcfft_forward_workspace_bytes_io(int64_t n_tokens, int in_features, int out_features, int block_size,
