@@ -83,13 +83,13 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
   // ---- x of token `wave` of M-tile m -> its slot by LDS-DMA (the buffer range zero-fills
   // tokens past n_tokens); piece q = rows 4q + (lane >> 4), 256 B each, with the slot's unit
   // swizzle (unit u of block row r at u ^ (r & 15)) applied to the global source offsets
-  auto dma_token = [&](int64_t m, char* region) {
-    const int64_t tok = m * TT + wave;
+  auto dma_token = [&](int64_t m, char* region, int sl) {
+    const int64_t tok = m * TT + sl;
     const bool ok = tok < n_tokens;
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<char*>((const char*)xv) + (ok ? tok : 0) * K * ES, 0, ok ? K * ES : 0, 0x00020000);
     const int dl = opaque(lane);
-    const uint32_t dst0 = lds_base + (uint32_t)(region - lds) + wave * SLOT;
+    const uint32_t dst0 = lds_base + (uint32_t)(region - lds) + sl * SLOT;
     int vb[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -105,7 +105,14 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
   };
 
   // ---- prologue: first tile's x, the DFT table, the stationary B fragments
-  if (wg_in_grp < n_mtiles) dma_token(wg_in_grp, lds);
+#ifdef BCFFT_DM8_FI
+  if (wg_in_grp < n_mtiles && wave < 4) {
+    dma_token(wg_in_grp, lds, wave);
+    dma_token(wg_in_grp, lds, wave + 4);
+  }
+#else
+  if (wg_in_grp < n_mtiles) dma_token(wg_in_grp, lds, wave);
+#endif
   {
     const uint4* tab = reinterpret_cast<const uint4*>(kDmF);
 #pragma unroll
@@ -139,10 +146,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
   lds_barrier();
 
   // ---- stage 1 (wave w, token slot w): x rows -> X units (one fp16 term), in place, per half
-  auto stage1 = [&](char* region, int par) {
+  auto stage1 = [&](char* region, int par, int sl) {
     const int l = opaque(lane);
     const int b16 = l & 15, g = l >> 4;
-    char* slot = region + wave * SLOT;
+    char* slot = region + sl * SLOT;
     // transposed-read lane address of the table: row 8g + q (+ 32 ks + 4 sec), chunk
     // (8 par + 2 mt + (p >> 1)) ^ fsw(row) = (8 par + 2 mt) ^ cx
     const int q4 = (l & 15) >> 2, p4 = l & 3;
@@ -185,7 +192,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
           }
       const float mxf = __builtin_fmaxf(m0, m1);
       const int sx = stat_scale_exp(2.f * __uint_as_float(wave_umax(__float_as_uint(mxf))));   // |a|, |d| <= 2 max|x|
-      if (l == 0) wsc[par * 16 + wave * 2 + h] = sx - 7;    // X = D 2^-(sx - 7): the table's 2^-7
+      if (l == 0) wsc[par * 16 + sl * 2 + h] = sx - 7;      // X = D 2^-(sx - 7): the table's 2^-7
       const float S = __int_as_float((sx + 127) << 23);
       f32x4 acc[8];
 #pragma unroll
@@ -300,11 +307,11 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
   // ---- stage 3 (wave w, token slot w of the previous tile): Y -> y rows staged in the slot
   // (32 rows x 256 B; GLU: 16 h rows) and stored as 1 KiB buffer stores. The slot's Y units are
   // read into registers first.
-  auto stage3 = [&](char* region, int par, int64_t mp) {
+  auto stage3 = [&](char* region, int par, int64_t mp, int sl) {
     const int l = opaque(lane);
     const int o16 = l & 15, g = l >> 4;
-    char* slot = region + wave * SLOT;
-    const int* sc = wsc + par * 16 + wave * 2;
+    char* slot = region + sl * SLOT;
+    const int* sc = wsc + par * 16 + sl * 2;
     const int nmin = min(sc[0], sc[1]);
     float ysc[NT];                                  // output block o = 16 nt + o16: 1 / s_o
 #pragma unroll
@@ -332,7 +339,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
     f16x8 gcur[KS][2], gnxt[KS][2];
     gload(0, gcur);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // Y is in registers: the slot is free
-    const int64_t tok = mp * TT + wave;
+    const int64_t tok = mp * TT + sl;
     const bool tok_ok = tok < n_tokens;
     const int nvalid = n_out - grp_o * OPG;
     // staging write bases: row o = 16 nt + o16, 8-B unit (4 mt + g + 16 hf) ^ sg
@@ -449,22 +456,50 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
     const bool have = m < n_mtiles;
     const int sb = 1 + 6 * (it < 9 ? it : 9);       // stamp slots: iterations 0-8, then the latest
     STAMP(sb);
+#ifdef BCFFT_DM8_FI
+    // F waves 0-3: stage 1 of tokens w and w + 4; I waves 4-7: stage 3 of tokens w - 4 and w of
+    // the previous tile (each SIMD then mixes one F and one I wave); the F waves stream the next
+    // tile's x for their two slots after Ba (the I waves' staging reads of those slots are done)
+    const bool fwave = wave < 4;
+    if (fwave) {
+      if (have) {
+        wait_vmcnt<0>();                            // this wave's own x DMA
+        STAMP(sb + 1);
+        stage1(region, par, wave);
+        stage1(region, par, wave + 4);
+      }
+    } else if (it > 0) {
+      stage3(other, par ^ 1, m - gstride, wave - 4);
+      stage3(other, par ^ 1, m - gstride, wave);
+    }
+    STAMP(sb + 2);
+    STAMP(sb + 3);
+    if (!have) break;
+    lds_barrier();                                  // Ba: X units and scales complete
+    STAMP(sb + 4);
+    if (fwave && m + gstride < n_mtiles) {
+      dma_token(m + gstride, other, wave);
+      dma_token(m + gstride, other, wave + 4);
+    }
+    stage2(region, par);
+#else
     if (have) {
       wait_vmcnt<0>();                              // this wave's x (and its older y stores)
       STAMP(sb + 1);
-      stage1(region, par);
+      stage1(region, par, wave);
     }
     STAMP(sb + 2);
-    if (it > 0) stage3(other, par ^ 1, m - gstride);
+    if (it > 0) stage3(other, par ^ 1, m - gstride, wave);
     if (m + gstride < n_mtiles) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
-      dma_token(m + gstride, other);
+      dma_token(m + gstride, other, wave);
     }
     STAMP(sb + 3);
     if (!have) break;
     lds_barrier();                                  // Ba: X units and scales complete
     STAMP(sb + 4);
     stage2(region, par);
+#endif
     lds_barrier();                                  // Bb: Y units complete
     STAMP(sb + 5);
   }
