@@ -29,6 +29,13 @@
 #include "bcfft_dm_table.h"
 #include "bcfft_dm_common.h"
 
+// stage 1 loads both quarters of a token's chunk before their two wave reductions, which then
+// interleave (bit-identical; 2-3 % faster at N = 1024 and 8192, tools/ab_dm64k.py);
+// -DBCFFT_DM64K_NO_ILP builds the quarter-by-quarter order for A/B
+#ifndef BCFFT_DM64K_NO_ILP
+#define BCFFT_DM64K_ILP
+#endif
+
 namespace bcfft {
 
 namespace dm64k {
@@ -178,8 +185,53 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
     for (int t2 = 0; t2 < 2; ++t2) {
       const int tl = wave + 8 * t2;
       char* slot = region + tl * XSLOT;
+#ifdef BCFFT_DM64K_ILP
+      // both quarters' x and maxima first, so their two wave reductions (DPP + readlane chains)
+      // can interleave; the per-quarter scales, and so every result, are unchanged
+      float xq2[KC][2][8];
+      int sxq[KC];
 #pragma unroll
       for (int h = 0; h < KC; ++h) {
+        const char* rowp = slot + (16 * h + b16) * (B * ES);
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt) {
+          const uint4 w = *reinterpret_cast<const uint4*>(rowp + 16 * ((g + 4 * pt) ^ (b16 & 7)));
+          const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float2 f = unpack16<XT>(ww[e]);
+            xq2[h][pt][2 * e] = f.x;
+            xq2[h][pt][2 * e + 1] = f.y;
+          }
+        }
+      }
+      uint32_t mq[KC];
+#pragma unroll
+      for (int h = 0; h < KC; ++h) {
+        float m0 = 0.f, m1 = 0.f;
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+          for (int j = 0; j < 8; j += 4) {
+            m0 = amax3(m0, xq2[h][pt][j], xq2[h][pt][j + 1]);
+            m1 = amax3(m1, xq2[h][pt][j + 2], xq2[h][pt][j + 3]);
+          }
+        mq[h] = __float_as_uint(__builtin_fmaxf(m0, m1));
+      }
+#pragma unroll
+      for (int h = 0; h < KC; ++h) mq[h] = wave_umax(mq[h]);
+#pragma unroll
+      for (int h = 0; h < KC; ++h) {
+        sxq[h] = stat_scale_exp(2.f * __uint_as_float(mq[h])) - HEAD;
+        if (l == 0) wsc[tl * 2 + h] = sxq[h] - 7;  // X = D 2^-(sx - 7): the table's 2^-7
+      }
+#endif
+#pragma unroll
+      for (int h = 0; h < KC; ++h) {
+#ifdef BCFFT_DM64K_ILP
+        float (&xq)[2][8] = xq2[h];
+        const int sx = sxq[h];
+#else
         float xq[2][8];
         const char* rowp = slot + (16 * h + b16) * (B * ES);
 #pragma unroll
@@ -204,6 +256,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
         const float mxf = __builtin_fmaxf(m0, m1);
         const int sx = stat_scale_exp(2.f * __uint_as_float(wave_umax(__float_as_uint(mxf)))) - HEAD;
         if (l == 0) wsc[tl * 2 + h] = sx - 7;      // X = D 2^-(sx - 7): the table's 2^-7
+#endif
         const float S = __int_as_float((sx + 127) << 23);
         uint32_t ah[4], dh[4];
 #pragma unroll
