@@ -160,8 +160,57 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
     int xwb[2];
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) xwb[pr] = 256 * g + 64 * (pr ^ (g & 1)) + 4 * b16;
+#ifdef BCFFT_S1_ILP
+    // both halves' x (packed) and maxima first, so their two wave reductions interleave; the
+    // per-half scales, and so every result, are unchanged
+    uint4 rawx[2][2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt)
+          rawx[h][ks][pt] = *reinterpret_cast<const uint4*>(slot + (16 * h + b16) * (B * ES) + 16 * ((4 * ks + g + 8 * pt) ^ b16));
+    uint32_t mxq[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
+      float m0f = 0.f, m1f = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt) {
+          const uint4 w = rawx[h][ks][pt];
+          const float2 f0 = unpack16<XT>(w.x), f1 = unpack16<XT>(w.y), f2 = unpack16<XT>(w.z), f3 = unpack16<XT>(w.w);
+          m0f = amax3(m0f, f0.x, f0.y);
+          m1f = amax3(m1f, f1.x, f1.y);
+          m0f = amax3(m0f, f2.x, f2.y);
+          m1f = amax3(m1f, f3.x, f3.y);
+        }
+      mxq[h] = __float_as_uint(__builtin_fmaxf(m0f, m1f));
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) mxq[h] = wave_umax(mxq[h]);
+#endif
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#ifdef BCFFT_S1_ILP
+      float xv8[2][2][8];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt) {
+          const uint4 w = rawx[h][ks][pt];
+          const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float2 f = unpack16<XT>(ww[e]);
+            xv8[ks][pt][2 * e] = f.x;
+            xv8[ks][pt][2 * e + 1] = f.y;
+          }
+        }
+      const int sx = stat_scale_exp(2.f * __uint_as_float(mxq[h]));
+      if (l == 0) wsc[par * 16 + sl * 2 + h] = sx - 7;
+#else
       // x of blocks 16h + b16: t = 32 ks + 8 g + j and t + 64 (j < 8); the half's x rows are
       // exactly the bytes its X units replace
       float xv8[2][2][8];
@@ -193,6 +242,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
       const float mxf = __builtin_fmaxf(m0, m1);
       const int sx = stat_scale_exp(2.f * __uint_as_float(wave_umax(__float_as_uint(mxf))));   // |a|, |d| <= 2 max|x|
       if (l == 0) wsc[par * 16 + sl * 2 + h] = sx - 7;      // X = D 2^-(sx - 7): the table's 2^-7
+#endif
       const float S = __int_as_float((sx + 127) << 23);
       f32x4 acc[8];
 #pragma unroll

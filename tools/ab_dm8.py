@@ -35,6 +35,13 @@ def main():
     x = torch.randn(256, h, device="cuda").to(torch.bfloat16)
     res["glu_N256"] = timed(lambda: ops.forward_glu(x, sgu, b, f), 50)
     outs["h256"] = ops.forward_glu(x, sgu, b, f).cpu()
+    # the multi-group kernels at N = 8192: config 2 (4096 -> 11008) and the fused gate/up
+    sup = ops.spectra((torch.randn(f // b, h // b, b) * 0.01).cuda())
+    x = torch.randn(8192, h, device="cuda").to(torch.bfloat16)
+    res["up_N8192"] = timed(lambda: ops.forward(x, sup, None, b, f), 30)
+    outs["up8192"] = ops.forward(x, sup, None, b, f).cpu()
+    res["glu_N8192"] = timed(lambda: ops.forward_glu(x, sgu, b, f), 30)
+    outs["h8192"] = ops.forward_glu(x, sgu, b, f).cpu()
     os.makedirs(out, exist_ok=True)
     torch.save(outs, os.path.join(out, tag + ".pt"))
     print(json.dumps({"lib": tag, "us": res}), flush=True)
