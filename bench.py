@@ -330,8 +330,8 @@ def load_traffic(tag, kernel, algo=None):
             continue
         e = d.get(tag)
         if e and e.get("kernel") == kernel and (algo is None or e.get("algo", algo) == algo):
-            return e.get("hbm_bytes_per_launch")
-    return None
+            return e.get("hbm_bytes_per_launch"), os.path.relpath(f, ROOT)
+    return None, None
 
 
 def run_variants(dev, algo, steps):
@@ -525,10 +525,14 @@ def main(argv=None):
     if rank == 0:
         roofline = None
         if not stub:
+            # PMC-measured HBM bytes of this kernel on this workload, from the committed rocprofv3
+            # passes (FETCH_SIZE x 2 + WRITE_SIZE); the source file is reported beside the number
+            traffic, traffic_src = load_traffic(tag, kname[1], kname[0])
             gbs = nbytes / (kern * 1e-3) / 1e9
             roofline = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
-                        "traffic": load_traffic(tag, kname[1], kname[0]),
+                        "traffic": traffic,
+                        "traffic_source": traffic_src,
                         "kernel": kname[1], "kernel_ms": round(kern, 5),
                         "algorithmic_bytes_per_launch": nbytes,
                         "fp32_tflops": round(algo_flops(n_local, k, m, b) / (kern * 1e-3) / 1e12, 2),
