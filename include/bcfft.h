@@ -184,11 +184,21 @@ int bcfft_forward_glu_algo(const void* x, int x_dtype, int64_t n_tokens, int in_
  *          4096 < intermediate <= 127 * 128 (LLaMA-7B's 11008); else BCFFT_ERR_BLOCK. The output is
  *          bit-identical to SPLIT's where SPLIT runs the 8-token streamed-weight down kernel.
  *   SPLIT: bcfft_forward_glu into the caller's workspace (h), then bcfft_forward (AUTO engines).
- *   AUTO:  FUSED where it serves the geometry and its 8-token tiles fill at least 3/8 of the CUs
- *          (N >= 768 on MI355X's 256), else SPLIT (at small N the split form's per-group gate/up
- *          kernel spreads over more CUs: 34 vs 52.6 us at N = 256).
+ *   AUTO:  on the fused geometry FUSED_SPLITK (below) at short grids, FUSED once its 8-token
+ *          tiles fill the CUs (last round >= 3/4 full), else SPLIT.
  * workspace: bcfft_forward_mlp_workspace_bytes(...) bytes (0 for FUSED; may then be NULL). */
-enum bcfft_mlp_mode { BCFFT_MLP_AUTO = 0, BCFFT_MLP_FUSED = 1, BCFFT_MLP_SPLIT = 2 };
+enum bcfft_mlp_mode { BCFFT_MLP_AUTO = 0, BCFFT_MLP_FUSED = 1, BCFFT_MLP_SPLIT = 2, BCFFT_MLP_FUSED_SPLITK = 3 };
+
+/* FUSED_SPLITK: the fused kernel with its gate/up groups (= the down projection's K-chunks) split
+ * over up to 6 workgroups per 8-token tile, each writing an fp32 partial y to the workspace
+ * (kz x n_tokens x hidden floats), plus a finishing pass that sums them in order and rounds: for
+ * short grids (decode, short prefill), where the one-launch kernel would leave most CUs idle.
+ * Deterministic; not bit-identical to FUSED / SPLIT (each slice has its own down-projection
+ * reference exponents). AUTO takes it where the fused geometry applies and FUSED's tiles would
+ * fill at most half the CUs (N <= 1024 on 256 CUs: 17-50 us vs 52-57 us one launch), FUSED past
+ * that while its tiles fill the CUs. bcfft_forward_mlp_mode returns the mode a call resolves to. */
+int bcfft_forward_mlp_mode(int64_t n_tokens, int hidden_features, int inter_features, int block_size, int x_dtype,
+                           int mode);
 
 int64_t bcfft_forward_mlp_workspace_bytes(int64_t n_tokens, int hidden_features, int inter_features, int block_size,
                                           int x_dtype, int mode);

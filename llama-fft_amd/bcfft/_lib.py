@@ -22,7 +22,7 @@ ALGOS = {"auto": ALGO_AUTO, "mfma": ALGO_MFMA, "valu": ALGO_VALU, "stationary": 
          "dftx": ALGO_DFTX}
 DTYPE_CODE = {torch.float32: BCFFT_F32, torch.float16: BCFFT_F16, torch.bfloat16: BCFFT_BF16}
 SUPPORTED_BLOCKS = (32, 64, 128, 256)
-MLP_MODES = {"auto": 0, "fused": 1, "split": 2}
+MLP_MODES = {"auto": 0, "fused": 1, "split": 2, "fused_splitk": 3}
 
 # every symbol include/bcfft.h declares, with its ctypes signature
 _SIGNATURES = {
@@ -54,6 +54,8 @@ _SIGNATURES = {
     "bcfft_forward_glu_algo": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
                                               ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                               ctypes.c_int, ctypes.c_void_p]),
+    "bcfft_forward_mlp_mode": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_int]),
     "bcfft_forward_mlp_workspace_bytes": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                           ctypes.c_int, ctypes.c_int]),
     "bcfft_forward_mlp": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int,

@@ -101,8 +101,10 @@ def forward_mlp(x2d: torch.Tensor, spec_gu: torch.Tensor, spec_down: torch.Tenso
     """y = BC_down(silu(BC_gate(x2d)) * BC_up(x2d)) (bcfft_forward_mlp): the LLaMA
     MLP as microbench_dense_vs_bc.py:183-188 times it. spec_gu = spectra(glu_weights(c_gate,
     c_up)), spec_down = spectra(c_down). mode "fused": one launch, h never written (bf16,
-    b = 128, hidden 4096, intermediate 4224..16256); "split": the gate/up + SwiGLU launch into a
-    workspace, then the down launch; "auto": fused where it applies. y has x2d's dtype and width."""
+    b = 128, hidden 4096, intermediate 4224..16256); "fused_splitk": the fused kernel with its
+    gate/up groups split over more workgroups at short grids (fp32 partials + a finishing pass);
+    "split": the gate/up + SwiGLU launch into a workspace, then the down launch; "auto": fused
+    where its tiles fill the CUs, fused_splitk at short grids, else split. y has x2d's dtype."""
     if mode not in _lib.MLP_MODES:
         raise ValueError(f"bcfft.forward_mlp: mode {mode!r}, expected one of {sorted(_lib.MLP_MODES)}")
     _lib.require_device(x2d, "bcfft.forward_mlp")
@@ -135,10 +137,11 @@ def mlp_fused_eligible(hidden_features: int, inter_features: int, block_size: in
 
 def mlp_auto_is_fused(n_tokens: int, hidden_features: int, inter_features: int, block_size: int,
                       dtype: torch.dtype) -> bool:
-    """Whether bcfft_forward_mlp's AUTO mode runs the one-launch kernel for these sizes (it needs
-    no workspace exactly then)."""
-    return _lib.load().bcfft_forward_mlp_workspace_bytes(n_tokens, hidden_features, inter_features, block_size,
-                                                         _lib.dtype_code(dtype), _lib.MLP_MODES["auto"]) == 0
+    """Whether bcfft_forward_mlp's AUTO mode runs the fused kernel for these sizes (one launch, or
+    its group split at short grids) rather than the gate/up launch and the down launch."""
+    mode = _lib.load().bcfft_forward_mlp_mode(n_tokens, hidden_features, inter_features, block_size,
+                                              _lib.dtype_code(dtype), _lib.MLP_MODES["auto"])
+    return mode in (_lib.MLP_MODES["fused"], _lib.MLP_MODES["fused_splitk"])
 
 
 def glu_eligible(in_features: int, block_size: int, dtype: torch.dtype | None = None) -> bool:

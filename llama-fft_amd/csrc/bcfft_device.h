@@ -626,6 +626,9 @@ void launch_dmk_image(int n_out, int n_in, void* spec, hipStream_t s);
 int dmk_ksplit(int64_t n, int n_in, int n_out);
 void launch_forward_dmk_split(const void* x, int64_t n, int n_in, int n_out, const void* spec, const void* bias,
                               int bias_dt, void* y, float* ws, int kz, hipStream_t s);
+// the split forms' finishing pass: y (bf16, n x M) = bf16(sum of the kz fp32 partial slabs in order) + bias
+void launch_partials_finish(const float* ws, int kz, int64_t n, int64_t M, const void* bias, int bias_dt, void* y,
+                            hipStream_t s);
 // fused BC-MLP (bcfft_dmm.hip): y = down(silu(gate(x)) * up(x)) in one launch; bf16 x and y,
 // b = 128, hidden 4096 (n_in = n_out = 32 blocks), intermediate n_h blocks with 32 < n_h <= 127
 bool dmm_eligible(int n_in, int b, int xdt, int n_h, int n_out);
@@ -635,6 +638,12 @@ bool dmm_eligible(int n_in, int b, int xdt, int n_h, int n_out);
 inline bool dmm_pays(int64_t n_tokens) { return multigroup_pays(n_tokens, 3); }
 void launch_mlp_dmm(const void* x, int64_t n, int n_h, const void* spec_gu, const void* spec_dn, void* y,
                     hipStream_t s);
+// its group split for short grids: kz slices of the gate/up groups (= the down projection's
+// K-chunks) per 8-token tile, fp32 partial y slabs (kz x n x 4096 floats) and the finishing
+// pass; dmm_ksplit: 1 = no split
+int dmm_ksplit(int64_t n, int n_h);
+void launch_mlp_dmm_split(const void* x, int64_t n, int n_h, const void* spec_gu, const void* spec_dn, void* y,
+                          float* ws, int kz, hipStream_t s);
 
 // weight prep (bcfft_prep.hip): loss-aware circulant projection of a dense (n_out*b, n_in*b)
 // weight into c (n_out, n_in, b) fp32; false for an unsupported block size

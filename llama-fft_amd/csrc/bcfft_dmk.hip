@@ -764,7 +764,11 @@ void launch_forward_dmk_split(const void* x, int64_t n, int n_in, int n_out, con
   const int64_t total = (int64_t)kz * groups * ((n + 7) / 8);
   hipLaunchKernelGGL((bc_forward_dmk_kernel<8, true>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat,
                      osc, nullptr, BCFFT_NONE, y, kz, ws);
-  const int64_t M = (int64_t)n_out * 128;
+  launch_partials_finish(ws, kz, n, (int64_t)n_out * 128, bias, bias_dt, y, s);
+}
+
+void launch_partials_finish(const float* ws, int kz, int64_t n, int64_t M, const void* bias, int bias_dt, void* y,
+                            hipStream_t s) {
   const int64_t quads = n * M / 4;
   const unsigned blocks = (unsigned)((quads + 255) / 256 < 4096 ? (quads + 255) / 256 : 4096);
   hipLaunchKernelGGL(bc_dmk_finish_kernel, dim3(blocks), dim3(256), 0, s, ws, kz, n, M, bias, bias_dt, (uint16_t*)y);

@@ -70,10 +70,14 @@ __device__ __forceinline__ uint32_t f16_pow2_neg(int d) {
 }
 }  // namespace dmm
 
+// SPL (short grids, dmm_ksplit): the gate/up groups (= the down projection's K-chunks) are split
+// into kz slices; workgroup b takes slice b % kz of exactly one 8-token tile and writes its partial
+// y in fp32 to ws[slice][token][column]; launch_partials_finish sums the slices and rounds.
+template <bool SPL>
 __global__ __launch_bounds__(512, 2) void bc_mlp_dmm_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_h, const uint32_t* __restrict__ gstat,
     const float* __restrict__ gosc, const uint32_t* __restrict__ dstat, const float* __restrict__ dosc,
-    void* __restrict__ yv) {
+    void* __restrict__ yv, int kz, float* __restrict__ ws) {
   using namespace dmm;
   constexpr int XT = BCFFT_BF16;
   constexpr int ES = 2;
@@ -92,7 +96,17 @@ __global__ __launch_bounds__(512, 2) void bc_mlp_dmm_kernel(
   const int n_groups = (n_h + OPG - 1) / OPG;       // gate/up groups = down K-chunks
   constexpr int64_t M = (int64_t)NOG * B;           // y row: 4096
   const int64_t n_mtiles = (n_tokens + TT - 1) / TT;
-  const int64_t gstride = gridDim.x;
+  // gate/up group range [g0, g1) of this workgroup; unsplit: all groups, persistent over tiles
+  int g0 = 0, g1 = n_groups, slice = 0;
+  int64_t m0 = blockIdx.x, gstride = gridDim.x;
+  if constexpr (SPL) {
+    slice = blockIdx.x % kz;
+    m0 = blockIdx.x / kz;
+    gstride = n_mtiles;                             // one tile per workgroup
+    const int gps = (n_groups + kz - 1) / kz;
+    g0 = slice * gps;
+    g1 = min(n_groups, g0 + gps);
+  }
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
   const uint4* gimg = reinterpret_cast<const uint4*>(gstat + 4);
   const uint4* dimg = reinterpret_cast<const uint4*>(dstat + 4);
@@ -137,9 +151,8 @@ __global__ __launch_bounds__(512, 2) void bc_mlp_dmm_kernel(
     bb[fb][nt] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, (fb * NT + nt) * 1024, 0);
   };
 
-  // ---- prologue: the first tile's x, the DFT table, the inverse weight scales, gate/up group 0's
+  // ---- prologue: the first tile's x, the DFT table, the inverse weight scales, gate/up group g0's
   // K-step 0 fragments
-  const int64_t m0 = blockIdx.x;
   dma_token(m0);
   {
     const uint4* tab = reinterpret_cast<const uint4*>(kDmF);
@@ -154,7 +167,7 @@ __global__ __launch_bounds__(512, 2) void bc_mlp_dmm_kernel(
   }
   wait_vmcnt<0>();
   {
-    const __amdgpu_buffer_rsrc_t rs = g_rsrc(0);
+    const __amdgpu_buffer_rsrc_t rs = g_rsrc(g0);
     const int vo = opaque(lane) * 16;
 #pragma unroll
     for (int fb = 0; fb < BW; ++fb)
@@ -574,6 +587,7 @@ __global__ __launch_bounds__(512, 2) void bc_mlp_dmm_kernel(
     const int l = opaque(lane);
     const int o16 = l & 15, g = l >> 4;
     char* slot = wr + wave * SLOT;
+    float* wsp = SPL ? ws + ((int64_t)slice * n_tokens + (tok < n_tokens ? tok : 0)) * M : nullptr;
     const int rref = wrr[wave];
     float ysc[NT];
 #pragma unroll
@@ -632,11 +646,18 @@ __global__ __launch_bounds__(512, 2) void bc_mlp_dmm_kernel(
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = hf ? fmaf(E[nt][r], ysc[nt], -os[r]) : fmaf(E[nt][r], ysc[nt], os[r]);
-          *reinterpret_cast<uint2*>(slot + 4096 * nt + swb[mt] + 128 * hf) =
-              make_uint2(pack16<XT>(v[0], v[1]), pack16<XT>(v[2], v[3]));
+          if constexpr (SPL) {                      // fp32 partial, 4 consecutive columns
+            if (tok_ok)
+              *reinterpret_cast<float4*>(wsp + (16 * nt + o16) * B + 16 * mt + 4 * g + 64 * hf) =
+                  make_float4(v[0], v[1], v[2], v[3]);
+          } else {
+            *reinterpret_cast<uint2*>(slot + 4096 * nt + swb[mt] + 128 * hf) =
+                make_uint2(pack16<XT>(v[0], v[1]), pack16<XT>(v[2], v[3]));
+          }
         }
       }
     }
+    if constexpr (SPL) return;
     constexpr int RB = B * ES;
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
         (char*)yv + (tok_ok ? tok : 0) * M * ES, 0, tok_ok ? (int)(M * ES) : 0, 0x00020000);
@@ -675,15 +696,15 @@ __global__ __launch_bounds__(512, 2) void bc_mlp_dmm_kernel(
     if (mprev >= 0) dn_stage3(mprev * TT + wave);
     lds_barrier();                                  // Ba: X units and exponents complete
     gu_factors();
-    for (int g = 0; g < n_groups; ++g) {
+    for (int g = g0; g < g1; ++g) {
       gu_stage2(g);
       lds_barrier();                                // Bb: Y units complete, XR reads done
-      if (g + 1 == n_groups && more_tiles) dma_token(m + gstride);
+      if (g + 1 == g1 && more_tiles) dma_token(m + gstride);
       gu_stage3(g);
       dn_stage1();
       lds_barrier();                                // Bd: the chunk's X units and exponents
-      const int gnext = g + 1 < n_groups ? g + 1 : (more_tiles ? 0 : -1);
-      if (g == 0) dn_stage2(std::true_type{}, gnext);
+      const int gnext = g + 1 < g1 ? g + 1 : (more_tiles ? g0 : -1);
+      if (g == g0) dn_stage2(std::true_type{}, gnext);
       else dn_stage2(std::false_type{}, gnext);
       lds_barrier();                                // Be: the chunk's X-unit reads done
     }
@@ -709,11 +730,37 @@ void launch_mlp_dmm(const void* x, int64_t n, int n_h, const void* spec_gu, cons
   const int64_t n_mtiles = (n + dmm::TT - 1) / dmm::TT;
   int64_t total = device_cu_count();
   if (total > n_mtiles) total = n_mtiles;
-  hipLaunchKernelGGL(bc_mlp_dmm_kernel, dim3((unsigned)total), dim3(512), 0, s, x, n, n_h,
+  hipLaunchKernelGGL(bc_mlp_dmm_kernel<false>, dim3((unsigned)total), dim3(512), 0, s, x, n, n_h,
                      reinterpret_cast<const uint32_t*>(spec_gu) + sg.stat_off_u32,
                      reinterpret_cast<const float*>(spec_gu) + sg.osc_off_u32,
                      reinterpret_cast<const uint32_t*>(spec_dn) + sd.stat_off_u32,
-                     reinterpret_cast<const float*>(spec_dn) + sd.osc_off_u32, y);
+                     reinterpret_cast<const float*>(spec_dn) + sd.osc_off_u32, y, 1, nullptr);
+}
+
+// group slices of the split form: where the one-launch kernel's tiles would fill at most half the
+// CUs, as many slices as fill them, >= 1 group each
+int dmm_ksplit(int64_t n, int n_h) {
+  const int64_t tiles = (n + dmm::TT - 1) / dmm::TT, cus = device_cu_count();
+  const int groups = (n_h + dmm::OPG - 1) / dmm::OPG;
+  if (n <= 0 || tiles * 2 > cus) return 1;
+  const int kz = (int)(cus / tiles < groups ? cus / tiles : groups);
+  if (kz < 2) return 1;
+  const int gps = (groups + kz - 1) / kz;
+  return (groups + gps - 1) / gps;                  // every slice non-empty
+}
+
+void launch_mlp_dmm_split(const void* x, int64_t n, int n_h, const void* spec_gu, const void* spec_dn, void* y,
+                          float* ws, int kz, hipStream_t s) {
+  const int groups = (n_h + dmm::OPG - 1) / dmm::OPG;
+  const SpecLayout sg = spec_layout(32 * groups, dmm::NI, 128);
+  const SpecLayout sd = spec_layout(dmm::NOG, n_h, 128);
+  const int64_t n_mtiles = (n + dmm::TT - 1) / dmm::TT;
+  hipLaunchKernelGGL(bc_mlp_dmm_kernel<true>, dim3((unsigned)(kz * n_mtiles)), dim3(512), 0, s, x, n, n_h,
+                     reinterpret_cast<const uint32_t*>(spec_gu) + sg.stat_off_u32,
+                     reinterpret_cast<const float*>(spec_gu) + sg.osc_off_u32,
+                     reinterpret_cast<const uint32_t*>(spec_dn) + sd.stat_off_u32,
+                     reinterpret_cast<const float*>(spec_dn) + sd.osc_off_u32, y, kz, ws);
+  launch_partials_finish(ws, kz, n, (int64_t)dmm::NOG * dmm::B, nullptr, BCFFT_NONE, y, s);
 }
 
 }  // namespace bcfft

@@ -944,26 +944,43 @@ int bcfft_forward_glu(const void* x, int x_dtype, int64_t n_tokens, int in_featu
                                 BCFFT_ALGO_AUTO, stream);
 }
 
-// the fused BC-MLP's resolved mode: FUSED where bcfft_dmm.hip serves the geometry (AUTO: once its
-// tiles fill enough CUs, bcfft::dmm_pays), else SPLIT; < 0 for invalid arguments
+// the fused BC-MLP's resolved mode: FUSED_SPLITK where bcfft_dmm.hip serves the geometry at a
+// short grid (bcfft::dmm_ksplit >= 2); FUSED where its tiles fill the CUs (bcfft::dmm_pays); else
+// SPLIT. Explicit modes are kept (a FUSED_SPLITK that would not
+// split runs as FUSED). < 0 for invalid arguments.
 static int mlp_mode(int64_t n_tokens, int hidden_features, int inter_features, int block_size, int x_dtype, int mode) {
-  if (mode != BCFFT_MLP_AUTO && mode != BCFFT_MLP_FUSED && mode != BCFFT_MLP_SPLIT) return -1;
+  if (mode != BCFFT_MLP_AUTO && mode != BCFFT_MLP_FUSED && mode != BCFFT_MLP_SPLIT && mode != BCFFT_MLP_FUSED_SPLITK)
+    return -1;
   if (!valid_block(block_size) || !valid_dt(x_dtype) || n_tokens < 0 || hidden_features <= 0 || inter_features <= 0 ||
       hidden_features % block_size || inter_features % block_size)
     return -1;
   const int n_hid = hidden_features / block_size, n_h = inter_features / block_size;
   const bool ok = bcfft::dmm_eligible(n_hid, block_size, x_dtype, n_h, n_hid);
-  if (mode == BCFFT_MLP_AUTO) return ok && bcfft::dmm_pays(n_tokens) ? BCFFT_MLP_FUSED : BCFFT_MLP_SPLIT;
+  const bool splits = ok && bcfft::dmm_ksplit(n_tokens, n_h) >= 2;
+  // AUTO: the group split wherever it applies (measured faster than the one launch up to its limit
+  // of half the CUs' worth of tiles: N = 1024 49.6 vs 56.7 us, N = 20 20.9 vs 52.0;
+  // profiles/r03p_mlp_time.log), the one launch where its tiles fill the CUs, else two launches
+  if (mode == BCFFT_MLP_AUTO)
+    return !ok ? BCFFT_MLP_SPLIT
+               : splits ? BCFFT_MLP_FUSED_SPLITK : bcfft::dmm_pays(n_tokens) ? BCFFT_MLP_FUSED : BCFFT_MLP_SPLIT;
+  if (mode == BCFFT_MLP_FUSED_SPLITK && ok && !splits) return BCFFT_MLP_FUSED;
   return mode;
 }
 
 static int64_t dt_bytes(int dt) { return dt == BCFFT_F32 ? 4 : 2; }
+
+int bcfft_forward_mlp_mode(int64_t n_tokens, int hidden_features, int inter_features, int block_size, int x_dtype,
+                           int mode) {
+  return mlp_mode(n_tokens, hidden_features, inter_features, block_size, x_dtype, mode);
+}
 
 int64_t bcfft_forward_mlp_workspace_bytes(int64_t n_tokens, int hidden_features, int inter_features, int block_size,
                                           int x_dtype, int mode) {
   const int m = mlp_mode(n_tokens, hidden_features, inter_features, block_size, x_dtype, mode);
   if (m < 0) return -1;
   if (m == BCFFT_MLP_FUSED) return 0;
+  if (m == BCFFT_MLP_FUSED_SPLITK)
+    return (int64_t)bcfft::dmm_ksplit(n_tokens, inter_features / block_size) * n_tokens * hidden_features * 4;
   return (n_tokens * (int64_t)inter_features * dt_bytes(x_dtype) + 15) / 16 * 16;   // h
 }
 
@@ -971,7 +988,8 @@ int bcfft_forward_mlp(const void* x, int x_dtype, int64_t n_tokens, int hidden_f
                       int block_size, const void* spectra_gu, const void* spectra_down, void* y, int mode,
                       void* workspace, int64_t workspace_bytes, void* stream) {
   g_last_detail[0] = 0;
-  if (mode != BCFFT_MLP_AUTO && mode != BCFFT_MLP_FUSED && mode != BCFFT_MLP_SPLIT) return BCFFT_ERR_ARG;
+  if (mode != BCFFT_MLP_AUTO && mode != BCFFT_MLP_FUSED && mode != BCFFT_MLP_SPLIT && mode != BCFFT_MLP_FUSED_SPLITK)
+    return BCFFT_ERR_ARG;
   if (!valid_block(block_size)) return refuse("bcfft_forward_mlp", BCFFT_ALGO_AUTO, 0, block_size, x_dtype, x_dtype);
   if (n_tokens < 0 || hidden_features <= 0 || inter_features <= 0 || hidden_features % block_size ||
       inter_features % block_size)
@@ -979,7 +997,7 @@ int bcfft_forward_mlp(const void* x, int x_dtype, int64_t n_tokens, int hidden_f
   if (!valid_dt(x_dtype)) return BCFFT_ERR_DTYPE;
   const int n_hid = hidden_features / block_size, n_h = inter_features / block_size;
   const int m = mlp_mode(n_tokens, hidden_features, inter_features, block_size, x_dtype, mode);
-  if (m == BCFFT_MLP_FUSED && !bcfft::dmm_eligible(n_hid, block_size, x_dtype, n_h, n_hid)) {
+  if ((m == BCFFT_MLP_FUSED || m == BCFFT_MLP_FUSED_SPLITK) && !bcfft::dmm_eligible(n_hid, block_size, x_dtype, n_h, n_hid)) {
     snprintf(g_last_detail, sizeof(g_last_detail),
              "bcfft_forward_mlp: the fused kernel serves bf16, block_size 128, hidden 4096 and intermediate "
              "4224..16256; got block_size %d, hidden %d, intermediate %d, x %s",
@@ -992,14 +1010,19 @@ int bcfft_forward_mlp(const void* x, int x_dtype, int64_t n_tokens, int hidden_f
       (workspace && !aligned16(workspace)))
     return BCFFT_ERR_ALIGN;
   hipStream_t s = (hipStream_t)stream;
+  const int64_t need = bcfft_forward_mlp_workspace_bytes(n_tokens, hidden_features, inter_features, block_size,
+                                                         x_dtype, m);
   if (m == BCFFT_MLP_FUSED) {
     bcfft::launch_mlp_dmm(x, n_tokens, n_h, spectra_gu, spectra_down, y, s);
     return record_launch();
   }
-  // SPLIT: h = silu(gate(x)) * up(x) into the workspace, then down(h) (two launches, AUTO engines)
-  const int64_t need = bcfft_forward_mlp_workspace_bytes(n_tokens, hidden_features, inter_features, block_size,
-                                                         x_dtype, BCFFT_MLP_SPLIT);
   if (!workspace || workspace_bytes < need) return BCFFT_ERR_ARG;
+  if (m == BCFFT_MLP_FUSED_SPLITK) {
+    bcfft::launch_mlp_dmm_split(x, n_tokens, n_h, spectra_gu, spectra_down, y, (float*)workspace,
+                                bcfft::dmm_ksplit(n_tokens, n_h), s);
+    return record_launch();
+  }
+  // SPLIT: h = silu(gate(x)) * up(x) into the workspace, then down(h) (two launches, AUTO engines)
   int st = bcfft_forward_glu(x, x_dtype, n_tokens, hidden_features, inter_features, block_size, spectra_gu, workspace,
                              stream);
   if (st != BCFFT_OK) return st;

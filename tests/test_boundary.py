@@ -208,8 +208,16 @@ def test_mlp_mode_and_workspace_without_gpu(built_lib):
     AUTO, FUSED, SPLIT = (_lib.MLP_MODES[m] for m in ("auto", "fused", "split"))
     F32, BF16 = _lib.BCFFT_F32, _lib.BCFFT_BF16
     assert wb(8192, 4096, 11008, 128, BF16, AUTO) == 0
-    assert wb(768, 4096, 11008, 128, BF16, AUTO) == 0                  # 96 tiles = 3/8 of 256 CUs
-    assert wb(760, 4096, 11008, 128, BF16, AUTO) == 760 * 11008 * 2      # fewer: the split form
+    assert wb(768, 4096, 11008, 128, BF16, AUTO) == 2 * 768 * 4096 * 4  # 96 tiles: group split, 2 slices
+    assert wb(1100, 4096, 11008, 128, BF16, AUTO) == 0                 # 138 tiles: one launch
+    assert wb(760, 4096, 11008, 128, BF16, AUTO) == 2 * 760 * 4096 * 4   # fewer: group split, 2 slices
+    assert wb(20, 4096, 11008, 128, BF16, AUTO) == 6 * 20 * 4096 * 4     # decode: 6 slices of 1 group
+    FSK = _lib.MLP_MODES["fused_splitk"]
+    mm = lib.bcfft_forward_mlp_mode
+    assert mm(20, 4096, 11008, 128, BF16, AUTO) == FSK and mm(8192, 4096, 11008, 128, BF16, AUTO) == FUSED
+    assert mm(2380, 4096, 11008, 128, BF16, AUTO) == SPLIT and mm(20, 4096, 11008, 128, F32, AUTO) == SPLIT
+    assert mm(8192, 4096, 11008, 128, BF16, FSK) == FUSED                # nothing to split: one launch
+    assert wb(20, 4096, 11008, 128, BF16, FUSED) == 0 and wb(20, 4096, 11008, 128, BF16, SPLIT) == 20 * 11008 * 2
     assert wb(2380, 4096, 11008, 128, BF16, AUTO) == 2380 * 11008 * 2    # 298 tiles: 2 thin rounds
     assert wb(3072, 4096, 11008, 128, BF16, AUTO) == 0                   # 2 rounds of 192 tiles
     assert wb(1, 4096, 11008, 128, BF16, FUSED) == 0
@@ -218,8 +226,8 @@ def test_mlp_mode_and_workspace_without_gpu(built_lib):
     assert wb(5, 4096, 11008, 64, BF16, AUTO) == 5 * 11008 * 2                      # b = 64: split
     assert wb(5, 4096, 4096, 128, BF16, AUTO) == 5 * 4096 * 2                       # 32 h blocks: split
     assert wb(5, 4096, 16384, 128, BF16, AUTO) == 5 * 16384 * 2                     # 128 h blocks: split
-    assert wb(1024, 4096, 16256, 128, BF16, AUTO) == 0                              # 127 h blocks
-    assert wb(5, 4096, 11008, 128, BF16, 3) == -1
+    assert wb(2048, 4096, 16256, 128, BF16, AUTO) == 0                              # 127 h blocks
+    assert wb(5, 4096, 11008, 128, BF16, 4) == -1
     assert wb(5, 4000, 11008, 128, BF16, AUTO) == -1
     fake = 4096
     fm = lib.bcfft_forward_mlp

@@ -38,10 +38,11 @@ def main():
     for n in ns:
         x = torch.randn(n, h, device="cuda").to(torch.bfloat16)
         y = torch.empty(n, h, device="cuda", dtype=torch.bfloat16)
-        wsb = lib.bcfft_forward_mlp_workspace_bytes(n, h, f, b, BF16, _lib.MLP_MODES["split"])
+        wsb = max(lib.bcfft_forward_mlp_workspace_bytes(n, h, f, b, BF16, _lib.MLP_MODES[m])
+                  for m in ("split", "fused_splitk"))
         ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
         out = {}
-        for mode in ("fused", "split"):
+        for mode in ("fused", "split", "fused_splitk"):
             code = _lib.MLP_MODES[mode]
 
             def call():
