@@ -45,6 +45,17 @@ def test_gpus2_launches_two_ranks(partition, per_rank, total, scaling):
     assert g["ms_per_step"] >= d["ms_per_step"] * 0.5 and g["value"] > 0
 
 
+def test_gpus4_global_partition():
+    """Four gloo ranks, as the driver's N=4 scaling run: the global batch splits 4 ways."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--partition", "global",
+                          *ARGS], capture_output=True, text=True, timeout=300, env=_env())
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = _line(out.stdout)
+    assert d["n_gpus"] == 4 and d["scaling"] == "strong"
+    assert d["config"]["tokens_per_rank"] == 50 and d["config"]["global_tokens"] == 200
+    assert d["value"] > 0 and d["with_allgather"]["value"] > 0
+
+
 def test_gpus1_single_process():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", *ARGS],
                          capture_output=True, text=True, timeout=300, env=_env())
