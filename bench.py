@@ -51,63 +51,47 @@ def algo_bytes(n, k, m, b, io, bias):
     return n * k * SZ[io] + n * m * SZ[io] + n_out * n_in * (b // 2 + 1) * 8 + (m * SZ[io] if bias else 0)
 
 
-def resolved_kernel(algo, k, b, io="fp32", m=4096):
-    """(algorithm, kernel symbol, MAC arithmetic) that BCFFT_ALGO=algo runs for this geometry and
-    I/O dtype (the output has the I/O dtype); mirrors bcfft_forward_algo's AUTO rule
-    (resolve_algo in csrc/bcfft_kernels.hip): at b = 128, K = 4096 fp32 outputs take dftx."""
-    n_in = k // b
-    if algo == "auto" and b == 128 and n_in == 32 and io == "fp32":
-        algo = "dftx"
-    stat_ok = (b == 128 and n_in == 32) or (b == 64 and n_in in (32, 64))
-    dft_ok = b == 128 and n_in == 32
-    if io == "bf16" and algo in ("dft", "auto") and b == 64 and 64 < n_in <= 255:
-        return ("dft", "bc_forward_dm64k_kernel",
-                "MFMA fp16 throughout, b=64, 16 tokens per tile, 32-block K-chunks with weight fragments "
-                "streamed from L2 (bf16 I/O)")
-    if io == "bf16" and algo in ("dft", "auto") and b == 64 and n_in == 64 and m > 64 * b:
-        return ("dft", "bc_forward_dm64g_kernel",
-                "MFMA fp16 throughout, b=64, 8 tokens per tile, stage 1 once per tile, every output group's "
-                "weight fragments streamed from L2 (bf16 I/O)")
-    if io == "bf16" and algo in ("dft", "auto") and b == 64 and n_in == 64:
-        return ("dft", "bc_forward_dm64_kernel",
-                "MFMA fp16 throughout, b=64, 8 tokens per tile, one-term spectra (bf16 I/O)")
-    if io == "bf16" and algo in ("dft", "auto") and b == 256 and n_in == 16 and m > 32 * b:
-        return ("dft", "bc_forward_dm256g_kernel",
-                "MFMA fp16 throughout, b=256 as three 128-point virtual rows, stage 1 once per 8-token tile, "
-                "every output group's weight fragments streamed from L2 (bf16 I/O)")
-    if io == "bf16" and algo in ("dft", "auto") and b == 256 and n_in == 16:
-        return ("dft", "bc_forward_dm256_kernel",
-                "MFMA fp16 throughout, b=256 as three 128-point virtual rows, 8 tokens per tile, "
-                "16 output blocks per workgroup (bf16 I/O)")
-    if io == "bf16" and algo in ("dft", "auto") and b == 256 and 1 <= n_in <= 127:
-        return ("dft", "bc_forward_dm256k_kernel",
-                "MFMA fp16 throughout, b=256 as three 128-point virtual rows, 16-block K-chunks with "
-                "weight fragments streamed from L2 (bf16 I/O)")
-    if io == "bf16" and algo in ("dft", "auto") and dft_ok and m > 32 * b:
-        return ("dft", "bc_forward_dmg_kernel",
-                "MFMA fp16 throughout, 8 tokens per tile, stage 1 once per tile, every output group's "
-                "weight fragments streamed from L2 (bf16 I/O)")
-    if io == "bf16" and algo in ("dft", "auto") and dft_ok:
-        return ("dft", "bc_forward_dm8_kernel",
-                "MFMA fp16 throughout, 8 tokens per tile, one-term spectra (bf16 I/O)")
-    if io == "bf16" and algo in ("dft", "auto") and b == 128 and 32 < n_in <= 127:   # N >= 32 (bench: 8192)
-        return ("dft", "bc_forward_dmk_kernel",
-                "MFMA fp16 throughout, 16-block K-chunks with weight fragments streamed from L2 (bf16 I/O)")
-    if algo == "dftx":
-        return ("dftx", "bc_forward_dm_kernel",
-                "MFMA fp16 throughout: block DFT (even/odd split, x hi+lo) x 2^-7 table, stationary "
-                "conj(C)*s_C MAC (X hi+lo), inverse DFT of Y hi+lo; f32 accumulate")
-    if algo == "dft" or (algo == "auto" and dft_ok):
-        return ("dft", "bc_forward_dm_kernel",
-                "MFMA fp16 throughout: block DFT (even/odd split, x hi+lo) x 2^-7 table, stationary "
-                "conj(C)*s_C MAC (X hi+lo), inverse DFT (Y one fp16 term); f32 accumulate")
-    if algo == "stationary" or (algo == "auto" and stat_ok):
-        return ("stationary", "bc_forward_stat_kernel",
-                "MFMA fp16: conj(C)*s_C (VGPR-resident) x per-token-scaled X split hi+lo, f32 accumulate")
-    if algo == "mfma" or (algo == "auto" and b <= 128):
-        return ("mfma", "bc_forward_mfma_kernel",
-                "MFMA bf16 hi/lo split (Xhi+Xlo)(Chi+Clo), f32 accumulate")
-    return ("valu", "bc_forward_valu_kernel", "VALU fp32 FMA")
+MAC = {
+    "bc_forward_dm_kernel": "MFMA fp16 throughout: block DFT (even/odd split, x hi+lo) x 2^-7 table, stationary "
+                            "conj(C)*s_o MAC (X hi+lo; s_o per output block), inverse DFT; f32 accumulate",
+    "bc_forward_dm8_kernel": "MFMA fp16 throughout, 8 tokens per tile, one-term spectra (bf16 I/O)",
+    "bc_forward_dmg_kernel": "MFMA fp16 throughout, 8 tokens per tile, stage 1 once per tile, every output group's "
+                             "weight fragments streamed from L2 (bf16 I/O)",
+    "bc_forward_dmk_kernel": "MFMA fp16 throughout, 16-block K-chunks with weight fragments streamed from L2 (bf16 I/O)",
+    "bc_forward_dm64_kernel": "MFMA fp16 throughout, b=64, 8 tokens per tile, one-term spectra (bf16 I/O)",
+    "bc_forward_dm64g_kernel": "MFMA fp16 throughout, b=64, 8 tokens per tile, stage 1 once per tile, every output "
+                               "group's weight fragments streamed from L2 (bf16 I/O)",
+    "bc_forward_dm64k_kernel": "MFMA fp16 throughout, b=64, 16 tokens per tile, 32-block K-chunks with weight "
+                               "fragments streamed from L2 (bf16 I/O)",
+    "bc_forward_dm256_kernel": "MFMA fp16 throughout, b=256 as three 128-point virtual rows, 8 tokens per tile, "
+                               "16 output blocks per workgroup (bf16 I/O)",
+    "bc_forward_dm256g_kernel": "MFMA fp16 throughout, b=256 as three 128-point virtual rows, stage 1 once per "
+                                "8-token tile, every output group's weight fragments streamed from L2 (bf16 I/O)",
+    "bc_forward_dm256k_kernel": "MFMA fp16 throughout, b=256 as three 128-point virtual rows, 16-block K-chunks with "
+                                "weight fragments streamed from L2 (bf16 I/O)",
+    "bc_forward_stat_kernel": "MFMA fp16: conj(C)*s_o (VGPR-resident) x per-token-scaled X split hi+lo, f32 accumulate",
+    "bc_forward_mfma_kernel": "MFMA bf16 hi/lo split (Xhi+Xlo)(Chi+Clo), f32 accumulate",
+    "bc_forward_valu_kernel": "VALU fp32 FMA",
+}
+ALGO_NAMES = {0: "auto", 1: "mfma", 2: "valu", 3: "stationary", 4: "dft", 5: "dftx", 6: "dftp"}
+
+
+def resolved_kernel(algo, k, b, io="fp32", m=4096, n=8192):
+    """(algorithm, kernel symbol, MAC arithmetic) that BCFFT_ALGO=algo runs for this geometry, token
+    count and I/O dtype (the output has the I/O dtype): asked of the library itself
+    (bcfft_forward_resolve / bcfft_forward_kernel_name, include/bcfft.h), which follows the
+    launchers' own choices (per-group / multi-group / K-split forms by token count and CUs)."""
+    from bcfft import _lib
+    lib = _lib.load()
+    code = _lib.dtype_code(DT[io])
+    a = lib.bcfft_forward_resolve(n, k, m, b, _lib.ALGOS[algo], code, code)
+    name = lib.bcfft_forward_kernel_name(n, k, m, b, _lib.ALGOS[algo], code, code).decode()
+    if a < 0:
+        raise ValueError(f"BCFFT_ALGO={algo} does not serve {k}->{m} b={b} {io}")
+    mac = MAC.get(name, "")
+    if name == "bc_forward_dm_kernel":
+        mac += "; Y hi+lo" if ALGO_NAMES[a] == "dftx" else "; Y one fp16 term"
+    return ALGO_NAMES[a], name, mac
 
 
 def algo_flops(n, k, m, b):
@@ -178,9 +162,10 @@ def time_layer(layer, x, steps, warmup, barrier=None):
 
 
 def reduce_max(vals, dev, world):
-    """Elementwise max over ranks (the slowest rank sets every timed figure)."""
+    """Elementwise max over ranks (the slowest rank sets every timed figure); through the process
+    group whenever one exists (the RCCL test runs it at world size 1 too)."""
     t = torch.tensor([float(v) for v in vals], device=dev, dtype=torch.float64)
-    if world > 1:
+    if world > 1 or dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(v) for v in t.cpu()]
 
@@ -199,16 +184,17 @@ def run_partitioned(fwd, x_local, n_total, steps, warmup, world, barrier, dev, s
                     allgather=True, repeats=5):
     """The timed core every rank runs (GPU ranks over RCCL, and the gloo test on CPU stubs):
     settle, then W warmup + K timed steps of fwd on the rank's shard between barriers, the max
-    over ranks; `repeats` more K-step windows; with N > 1 and allgather, forward + the single
-    all-gather of the y shards (bcfft.shard.gather_rows) timed the same way. Returns
-    {wall, kern, reps (sorted), gather_wall or None}."""
+    over ranks; `repeats` more K-step windows; with a process group (N > 1, or the RCCL test's
+    single rank) and allgather, forward + the single all-gather of the y shards
+    (bcfft.shard.gather_rows) timed the same way. Returns {wall, kern, reps (sorted), gather_wall
+    or None}."""
     from bcfft.shard import gather_rows
     step = lambda: fwd(x_local)  # noqa: E731
     settle(step, settle_ms, dev)
     wall, kern = reduce_max(time_fn(step, steps, warmup, barrier, dev), dev, world)
     reps = sorted(reduce_max([time_fn(step, steps, 2, barrier, dev)[1] for _ in range(repeats)], dev, world))
     gather = None
-    if world > 1 and allgather:
+    if (world > 1 or dist.is_initialized()) and allgather:
         g = time_fn(lambda: gather_rows(fwd(x_local), n_total), steps, 3, barrier, dev)[0]
         gather = reduce_max([g], dev, world)[0]
     return {"wall": wall, "kern": kern, "reps": reps, "gather_wall": gather}
@@ -276,7 +262,7 @@ def time_glu(dev, steps, k=4096, m=11008, b=128, n=8192, io="bf16"):
         fused_stat = run(lambda: ops.forward_glu(x, sgu, b, m, algo="stationary")) if b <= 128 else None
         unfused = run(lambda: torch.nn.functional.silu(ops.forward(x, sg, None, b, m)) * ops.forward(x, su, None, b, m))
     nbytes = n * k * SZ[io] + n * m * SZ[io] + 2 * (m // b) * (k // b) * (b // 2 + 1) * 8
-    engine = "dft-glu" if resolved_kernel("auto", k, b, io)[0] in ("dft", "dftx") else "stationary-glu"
+    engine = "dft-glu" if resolved_kernel("auto", k, b, io, k, n)[0] in ("dft", "dftx") else "stationary-glu"
     return {"workload": f"gate/up {k}->{m} b={b} N={n} {io}-io + SwiGLU", "engine": engine,
             "ms": round(fused, 4), "stationary_glu_ms": None if fused_stat is None else round(fused_stat, 4),
             "unfused_ms": round(unfused, 4),
@@ -365,7 +351,7 @@ def run_variants(dev, algo, steps):
         del g
         vbytes = algo_bytes(vn, vk, vm, vb, vio, False)
         variants.append({"workload": f"{vk}->{vm} b={vb} N={vn} {vio}-io algo={va}",
-                         "engine": resolved_kernel(va, vk, vb, vio, vm)[1].replace("bc_forward_", "").replace("_kernel", ""),
+                         "engine": resolved_kernel(va, vk, vb, vio, vm, vn)[1].replace("bc_forward_", "").replace("_kernel", ""),
                          "ms": round(gk, 4),
                          "eager_ms": round(vkern, 4),
                          "GTok_elem_s": round(vn * vm / (gk * 1e-3) / 1e9, 3),
@@ -392,6 +378,32 @@ def host_cores():
     return n
 
 
+def cpu_model():
+    """The host CPU's model name and thread count (lscpu's "Model name" / "CPU(s)"), for the
+    cpu_baseline record: the CPU figure depends on which host the box landed on."""
+    name, threads = None, os.cpu_count()
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for ln in out.splitlines():
+            key, _, val = ln.partition(":")
+            if key.strip() == "Model name" and name is None:
+                name = val.strip()
+            elif key.strip() == "CPU(s)":
+                threads = int(val.strip())
+    except (OSError, ValueError, Exception):
+        pass
+    if name is None:
+        try:
+            for ln in open("/proc/cpuinfo"):
+                if ln.startswith("model name"):
+                    name = ln.split(":", 1)[1].strip()
+                    break
+        except OSError:
+            pass
+    return name, threads
+
+
 def cpu_baseline(k, m, b, io, bias, budget_s):
     """Oracle's torch-CPU restatement of the cached forward (bench_all_in_one.py:179-231),
     fp32, on a bounded token sample, on all the host cores this process may use; GTok-elem/s."""
@@ -413,10 +425,12 @@ def cpu_baseline(k, m, b, io, bias, budget_s):
         el = time.perf_counter() - t0
         if el >= budget_s or it >= 10000:
             break
+    model, host_threads = cpu_model()
     return {"value": round(n * m * it / el / 1e9, 5), "unit": "GTok-elem/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "cpu_model": model, "host_threads": host_threads,
             "sample": f"{it} x forward of {n} tokens, {k}->{m} b={b} fp32 (torch CPU rfft/einsum/"
-                      f"irfft, cached spectra), {el:.1f} s on {threads} threads"}
+                      f"irfft, cached spectra), {el:.1f} s on {threads} of the host's {host_threads} "
+                      f"threads ({model}); the box's CPU share (affinity / cgroup quota) sets `cores`"}
 
 
 def parse_args(argv=None):
@@ -517,7 +531,7 @@ def main(argv=None):
 
     spectra_ms = time_spectra(layer) if layer is not None else None
     tag = f"{k}x{m}_b{b}_n{n_local}_{io}"
-    kname = resolved_kernel(algo, k, b, io, m)
+    kname = resolved_kernel(algo, k, b, io, m, n_local) if not stub else ("stub", "stub", "CPU stub")
     cpu = None
     if rank == 0 and world == 1 and args.cpu_budget > 0 and not stub:
         cpu = cpu_baseline(k, m, b, io, bool(args.bias), args.cpu_budget)
@@ -567,6 +581,9 @@ def main(argv=None):
         }
         if stub:
             line["stub"] = args.stub
+        if world > 1 and args.partition == "global":
+            line["scaling_note"] = ("strong scaling: the global 8192 tokens split over the ranks; every rank's "
+                                    "shard runs the same kernel as N=1 on fewer tokens (1024 at N=8)")
         if gather:
             line["with_allgather"] = gather
         if variants:

@@ -118,6 +118,19 @@ int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_feat
                        int out_features, int block_size, const void* spectra, const void* bias,
                        int bias_dtype, void* y, int y_dtype, int algo, void* stream);
 
+/* The engine (enum bcfft_algo, AUTO resolved) that bcfft_forward_ws runs for these sizes and I/O
+ * dtypes with the workspace bcfft_forward_workspace_bytes_io asks for; < 0 where it would refuse
+ * the call. Host logic: nothing is launched. Replaces nothing in the reference (its forward has one
+ * code path); benchmarks and tests use it to name what they time. */
+int bcfft_forward_resolve(int64_t n_tokens, int in_features, int out_features, int block_size, int algo,
+                          int x_dtype, int y_dtype);
+
+/* The kernel symbol (e.g. "bc_forward_dm_kernel") that call runs: each launcher's own choice
+ * between its per-group, multi-group and K-split forms for the current device's CU count; ""
+ * where the call would be refused. */
+const char* bcfft_forward_kernel_name(int64_t n_tokens, int in_features, int out_features, int block_size,
+                                      int algo, int x_dtype, int y_dtype);
+
 /* Optional workspace of bcfft_forward_ws, in bytes (0: the forward never uses one; < 0:
  * invalid geometry). Non-zero only where the split-bf16 MFMA kernel or the VALU kernel (algo,
  * AUTO resolved) runs a grid too short to fill the device (MFMA: n_tokens < 8 x CUs) over >= 4

@@ -40,6 +40,10 @@ _SIGNATURES = {
                                           ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_void_p]),
+    "bcfft_forward_resolve": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_int]),
+    "bcfft_forward_kernel_name": (ctypes.c_char_p, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                    ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "bcfft_forward_workspace_bytes": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                        ctypes.c_int]),
     "bcfft_forward_workspace_bytes_io": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,

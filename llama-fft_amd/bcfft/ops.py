@@ -144,13 +144,30 @@ def mlp_auto_is_fused(n_tokens: int, hidden_features: int, inter_features: int, 
     return mode in (_lib.MLP_MODES["fused"], _lib.MLP_MODES["fused_splitk"])
 
 
-def glu_eligible(in_features: int, block_size: int, dtype: torch.dtype | None = None) -> bool:
-    """Geometries the fused gate/up kernel serves (include/bcfft.h): the stationary ones, and
-    b = 256 with K = 4096 for bf16 x (the b = 256 multi-group DFT kernel)."""
+def glu_eligible(in_features: int, block_size: int, dtype: torch.dtype | None = None, algo: str | None = None,
+                 gate_features: int | None = None) -> bool:
+    """Whether bcfft_forward_glu_algo serves this geometry with this engine (include/bcfft.h), so
+    callers fall back to two launches instead of meeting BCFFT_ERR_BLOCK. Mirrors the C rules:
+    b = 256 with K = 4096 only for bf16 x under auto / dft, up to 512 gate blocks (the kernel's
+    group limit); otherwise the stationary geometries, where dftx needs b = 128 with K = 4096 and
+    dft that or b = 64 with K = 4096 and bf16 x; mfma / valu have no fused form. algo None: the
+    BCFFT_ALGO environment (default auto)."""
+    algo = default_algo() if algo is None else algo
+    if algo in ("mfma", "valu") or block_size <= 0 or in_features % block_size:
+        return False
     n_in = in_features // block_size
     if block_size == 256 and n_in == 16:
-        return dtype == torch.bfloat16
-    return (block_size == 128 and n_in == 32) or (block_size == 64 and n_in in (32, 64))
+        n_gate = None if gate_features is None else gate_features // block_size
+        return (dtype == torch.bfloat16 and algo in ("auto", "dft")
+                and (n_gate is None or 2 * (-(-n_gate // 16)) <= 64))
+    dm = block_size == 128 and n_in == 32
+    dm64 = block_size == 64 and n_in == 64 and dtype == torch.bfloat16
+    stat = dm or (block_size == 64 and n_in in (32, 64))
+    if algo == "dftx":
+        return dm
+    if algo == "dft":
+        return dm or dm64
+    return stat
 
 
 def default_algo() -> str:

@@ -604,7 +604,8 @@ void launch_forward_dm8(const void* x, int64_t n, int n_out, const void* spec, c
 bool dm256_eligible(int n_in, int b, int xdt, bool yf32);
 void launch_forward_dm256(const void* x, int64_t n, int n_in, int n_out, const void* spec, const void* bias,
                           int bias_dt, void* y, hipStream_t s);
-bool dm256_glu_eligible(int n_in, int b, int xdt);
+bool dm256_glu_eligible(int n_in, int b, int xdt, int n_gate);
+const char* dm256_kernel_name(int64_t n, int n_in, int n_out);   // the kernel launch_forward_dm256 runs
 void launch_forward_dm256_glu(const void* x, int64_t n, int n_gate, const void* spec, void* h, hipStream_t s);
 // b = 64, K > 4096 (up to 255 input blocks), bf16 x and bf16 y (bcfft_dm64k.hip)
 bool dm64k_eligible(int n_in, int b, int xdt, bool yf32);

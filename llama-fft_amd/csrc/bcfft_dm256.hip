@@ -1470,6 +1470,21 @@ bool dm256_eligible(int n_in, int b, int xdt, bool yf32) {
   return dm256_geometry(n_in, b) && xdt == BCFFT_BF16 && !yf32;
 }
 
+// the multi-group kernel (stage 1 once per 8-token tile) serves K = 4096 from three output groups
+// of 16 blocks, up to MAXG, once its tiles fill the CUs (bcfft::multigroup_pays)
+bool dm256g_taken(int64_t n, int n_in, int n_out) {
+  const int groups = (n_out + d256::NOB - 1) / d256::NOB;
+#ifdef BCFFT_NO_DM256G
+  return false;
+#endif
+  return n_in == d256::NI && groups >= 3 && groups <= d256::MAXG && multigroup_pays(n, 3);
+}
+
+const char* dm256_kernel_name(int64_t n, int n_in, int n_out) {
+  return dm256g_taken(n, n_in, n_out) ? "bc_forward_dm256g_kernel"
+                                      : n_in == d256::NI ? "bc_forward_dm256_kernel" : "bc_forward_dm256k_kernel";
+}
+
 void launch_forward_dm256(const void* x, int64_t n, int n_in, int n_out, const void* spec, const void* bias,
                           int bias_dt, void* y, hipStream_t s) {
   const int groups = (n_out + d256::NOB - 1) / d256::NOB;
@@ -1478,14 +1493,12 @@ void launch_forward_dm256(const void* x, int64_t n, int n_in, int n_out, const v
   const int64_t total = group_grid(device_cu_count(), groups, n_mtiles);
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
   const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
-#ifndef BCFFT_NO_DM256G
-  if (n_in == d256::NI && groups >= 3 && groups <= d256::MAXG && multigroup_pays(n, 3)) {   // x transformed once
+  if (dm256g_taken(n, n_in, n_out)) {             // x transformed once
     const int64_t wgs = device_cu_count() < n_mtiles ? device_cu_count() : n_mtiles;
     hipLaunchKernelGGL(bc_forward_dm256g_kernel<false>, dim3((unsigned)wgs), dim3(512), 0, s, x, n, n_out, stat, osc,
                        bias, bias_dt, y);
     return;
   }
-#endif
   if (n_in == d256::NI)
     hipLaunchKernelGGL(bc_forward_dm256_kernel, dim3((unsigned)total), dim3(512), 0, s, x, n, n_out, stat, osc, bias,
                        bias_dt, y);
@@ -1498,7 +1511,11 @@ void launch_forward_dm256(const void* x, int64_t n, int n_in, int n_out, const v
 namespace bcfft {
 // fused gate/up + SwiGLU at b = 256, K = 4096, bf16 (the multi-group kernel's GLU form): spec
 // holds ceil(n_gate / 16) STAT groups of 16 gate + 16 up blocks
-bool dm256_glu_eligible(int n_in, int b, int xdt) { return b == 256 && n_in == d256::NI && xdt == BCFFT_BF16; }
+// the GLU form splits each 32-block group into two virtual groups of 16, whose inverse weight scales
+// the kernel stages in an LDS array of MAXG groups: 2 ceil(n_gate / 16) <= MAXG (n_gate <= 512 blocks)
+bool dm256_glu_eligible(int n_in, int b, int xdt, int n_gate) {
+  return b == 256 && n_in == d256::NI && xdt == BCFFT_BF16 && n_gate >= 1 && 2 * ((n_gate + 15) / 16) <= d256::MAXG;
+}
 
 void launch_forward_dm256_glu(const void* x, int64_t n, int n_gate, const void* spec, void* h, hipStream_t s) {
   const int stat_groups = (n_gate + 15) / 16;

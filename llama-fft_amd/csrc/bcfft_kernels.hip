@@ -887,6 +887,57 @@ int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_featur
   return record_launch();
 }
 
+// The engine and kernel bcfft_forward_ws runs for these arguments (with the workspace that
+// bcfft_forward_workspace_bytes_io asks for): the same refusals, resolve_algo, and each launcher's
+// own choice between its per-group, multi-group and split forms. Host logic only (no launch).
+static int forward_plan(int64_t n_tokens, int in_features, int out_features, int block_size, int algo, int x_dtype,
+                        int y_dtype, const char** kernel) {
+  *kernel = "";
+  if (!valid_block(block_size) || n_tokens < 0 || in_features <= 0 || out_features <= 0 ||
+      in_features % block_size || out_features % block_size)
+    return -1;
+  if (!valid_dt(x_dtype) || !valid_dt(y_dtype)) return -1;
+  if (algo < BCFFT_ALGO_AUTO || algo > BCFFT_ALGO_DFTX) return -1;
+  const int n_in = in_features / block_size, n_out = out_features / block_size;
+  const bool yf32 = y_dtype == BCFFT_F32;
+  const bool dm = bcfft::dm_eligible(n_in, block_size);
+  const bool dm64 = bcfft::dm64_eligible(n_in, block_size, x_dtype, yf32);
+  const bool dmk = bcfft::dmk_eligible(n_in, block_size, x_dtype, yf32);
+  const bool dm256 = bcfft::dm256_eligible(n_in, block_size, x_dtype, yf32);
+  const bool dm64k = bcfft::dm64k_eligible(n_in, block_size, x_dtype, yf32);
+  if (algo == BCFFT_ALGO_STAT && !bcfft::stat_eligible(n_in, block_size)) return -1;
+  if (algo == BCFFT_ALGO_DFTX && !dm) return -1;
+  if (algo == BCFFT_ALGO_DFT && !dm && !dm64 && !dmk && !dm256 && !dm64k) return -1;
+  const int a = resolve_algo(algo, n_in, block_size, x_dtype, yf32, n_tokens);
+  if (a == BCFFT_ALGO_DFT && dmk) *kernel = "bc_forward_dmk_kernel";
+  else if (a == BCFFT_ALGO_DFT && dm256) *kernel = bcfft::dm256_kernel_name(n_tokens, n_in, n_out);
+  else if (a == BCFFT_ALGO_DFT && dm64k) *kernel = "bc_forward_dm64k_kernel";
+  else if (a == BCFFT_ALGO_DFT && block_size == 64)
+    *kernel = bcfft::dm64g_eligible(64, 64, BCFFT_BF16, false, n_out, false) && bcfft::multigroup_pays(n_tokens, 4)
+                  ? "bc_forward_dm64g_kernel" : "bc_forward_dm64_kernel";
+  else if (a == BCFFT_ALGO_DFT && bcfft::dm8_eligible(n_in, block_size, x_dtype, yf32))
+    *kernel = bcfft::dmg_eligible(n_in, block_size, x_dtype, yf32, n_out, false) && bcfft::multigroup_pays(n_tokens, 3)
+                  ? "bc_forward_dmg_kernel" : "bc_forward_dm8_kernel";
+  else if (a == BCFFT_ALGO_DFT || a == BCFFT_ALGO_DFTX) *kernel = "bc_forward_dm_kernel";
+  else if (a == BCFFT_ALGO_STAT) *kernel = "bc_forward_stat_kernel";
+  else if (a == BCFFT_ALGO_MFMA && block_size <= BCFFT_MFMA_MAXB) *kernel = "bc_forward_mfma_kernel";
+  else *kernel = "bc_forward_valu_kernel";
+  return a;
+}
+
+int bcfft_forward_resolve(int64_t n_tokens, int in_features, int out_features, int block_size, int algo, int x_dtype,
+                          int y_dtype) {
+  const char* k;
+  return forward_plan(n_tokens, in_features, out_features, block_size, algo, x_dtype, y_dtype, &k);
+}
+
+const char* bcfft_forward_kernel_name(int64_t n_tokens, int in_features, int out_features, int block_size, int algo,
+                                      int x_dtype, int y_dtype) {
+  const char* k;
+  forward_plan(n_tokens, in_features, out_features, block_size, algo, x_dtype, y_dtype, &k);
+  return k;
+}
+
 int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_features,
                        int out_features, int block_size, const void* spectra, const void* bias,
                        int bias_dtype, void* y, int y_dtype, int algo, void* stream) {
@@ -905,7 +956,7 @@ int bcfft_forward_glu_algo(const void* x, int x_dtype, int64_t n_tokens, int in_
     return BCFFT_ERR_SHAPE;
   if (!valid_dt(x_dtype)) return BCFFT_ERR_DTYPE;
   const int n_in = in_features / block_size, n_gate = gate_features / block_size;
-  const bool g256 = bcfft::dm256_glu_eligible(n_in, block_size, x_dtype);   // b = 256, K = 4096, bf16
+  const bool g256 = bcfft::dm256_glu_eligible(n_in, block_size, x_dtype, n_gate);   // b = 256, K = 4096, bf16
   if (!bcfft::stat_eligible(n_in, block_size) && !g256)
     return refuse("bcfft_forward_glu", algo, n_in, block_size, x_dtype, x_dtype);
   if (g256) {

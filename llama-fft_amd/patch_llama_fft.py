@@ -374,10 +374,10 @@ class BCFusedGateUp(nn.Module):
     def _fused_ok(self, x: torch.Tensor) -> bool:
         g, u = self._gate, self._up
         grad = torch.is_grad_enabled() and (g.c.requires_grad or u.c.requires_grad or x.requires_grad)
-        # BCFFT_ALGO=mfma / valu asks for an exact engine, which has no fused form: two launches
+        # the fused launch only where bcfft_forward_glu_algo serves the geometry with the engine
+        # BCFFT_ALGO names (mfma / valu have no fused form): otherwise two launches, never an error
         return (g.bias is None and u.bias is None and not grad and x.is_cuda
-                and _ops.default_algo() not in ("mfma", "valu")
-                and _ops.glu_eligible(g.in_features, g.block_size, x.dtype))
+                and _ops.glu_eligible(g.in_features, g.block_size, x.dtype, _ops.default_algo(), g.out_features))
 
     def _spectra(self) -> torch.Tensor:
         g, u = self._gate.c, self._up.c

@@ -17,7 +17,9 @@ def test_algorithmic_bytes_match_survey():
     assert bench.algo_bytes(8192, 4096, 4096, 128, "bf16", False) == 134_750_208
 
 
-def test_engine_resolution_mirrors_auto_rule():
+def test_engine_resolution_mirrors_auto_rule(built_lib):
+    """bench.py names the kernel the library itself resolves (bcfft_forward_kernel_name): the AUTO
+    rule and each launcher's per-group / multi-group choice by token count (no GPU: 256 CUs)."""
     assert bench.resolved_kernel("auto", 4096, 128)[:2] == ("dftx", "bc_forward_dm_kernel")   # fp32 out
     assert bench.resolved_kernel("auto", 4096, 128, "fp16")[:2] == ("dft", "bc_forward_dm_kernel")
     assert bench.resolved_kernel("dft", 4096, 128)[:2] == ("dft", "bc_forward_dm_kernel")
@@ -31,6 +33,16 @@ def test_engine_resolution_mirrors_auto_rule():
     assert bench.resolved_kernel("auto", 4096, 64, "bf16", 11008)[1] == "bc_forward_dm64g_kernel"
     assert bench.resolved_kernel("auto", 2048, 64, "bf16")[1] == "bc_forward_stat_kernel"
     assert bench.resolved_kernel("valu", 4096, 128)[1] == "bc_forward_valu_kernel"
+    assert bench.resolved_kernel("auto", 4096, 128, "bf16", 11008, 8192)[1] == "bc_forward_dmg_kernel"
+    assert bench.resolved_kernel("auto", 4096, 128, "bf16", 11008, 20)[1] == "bc_forward_dm8_kernel"  # short grid
+    assert bench.resolved_kernel("auto", 11008, 128, "bf16", 4096, 8192)[1] == "bc_forward_dmk_kernel"
+    assert bench.resolved_kernel("auto", 11008, 64, "bf16", 4096, 8192)[1] == "bc_forward_dm64k_kernel"
+    assert bench.resolved_kernel("auto", 11008, 64, "bf16", 4096, 64)[1] == "bc_forward_mfma_kernel"  # < 128 tokens
+    assert bench.resolved_kernel("auto", 4096, 256, "bf16", 11008, 8192)[1] == "bc_forward_dm256g_kernel"
+    assert bench.resolved_kernel("auto", 4096, 256, "bf16", 11008, 20)[1] == "bc_forward_dm256_kernel"
+    assert bench.resolved_kernel("auto", 11008, 256, "bf16", 4096, 8192)[1] == "bc_forward_dm256k_kernel"
+    with pytest.raises(ValueError):
+        bench.resolved_kernel("dftx", 4096, 64)
 
 
 @pytest.mark.gpu

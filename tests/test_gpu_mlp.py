@@ -53,7 +53,10 @@ def _run(dev, x, cg, cu, cd, mode):
 
 
 def _silu(a):
-    return a / (1.0 + np.exp(-a.astype(np.float64)))
+    """a * sigmoid(a) in fp64 without overflow: exp of a non-positive argument only."""
+    a = a.astype(np.float64)
+    e = np.exp(-np.abs(a))
+    return a * np.where(a >= 0, 1.0 / (1.0 + e), e / (1.0 + e))
 
 
 def oracle_mlp(x, cg, cu, cd, dt=O.BF16):
