@@ -90,7 +90,9 @@ def resolved_kernel(algo, k, b, io="fp32", m=4096, n=8192):
         raise ValueError(f"BCFFT_ALGO={algo} does not serve {k}->{m} b={b} {io}")
     mac = MAC.get(name, "")
     if name == "bc_forward_dm_kernel":
-        mac += "; Y hi+lo" if ALGO_NAMES[a] == "dftx" else "; Y one fp16 term"
+        mac += {"dftx": "; Y hi+lo", "dftp": "; Y hi+lo, and every single fp16 term's rounding residual "
+                "(table, weight spectra) added back by fp8 MFMAs (e4m3 residual x bf8 operand)"}.get(
+                    ALGO_NAMES[a], "; Y one fp16 term")
     return ALGO_NAMES[a], name, mac
 
 

@@ -51,12 +51,17 @@ enum bcfft_dtype { BCFFT_NONE = -1, BCFFT_F32 = 0, BCFFT_F16 = 1, BCFFT_BF16 = 2
  *        streamed from L2 per 16-block K-chunk (the LLaMA down projection; bcfft_dmk.hip).
  *  DFTX: DFT with the per-bin products also split hi + lo before the inverse transform:
  *        ~2.8e-4 relative and linear in x to ~1e-6, ~6 % slower.
+ *  DFTP: the precise engine: DFTX with the rounding residual of every single fp16 term (the DFT
+ *        table in both transforms and the weight spectra) added back through fp8 MFMAs into the
+ *        same fp32 accumulators: ~1e-5 relative, per token ~1e-5 times its cancellation (the
+ *        reference's fp32 arithmetic class). Geometry as DFTX; fp32 outputs (16-bit outputs run
+ *        DFTX, whose error already sits below their rounding).
  *  AUTO: at block_size 128 with in_features 4096, DFTX for fp32 outputs (linear in x, which the
  *        fp32 backward's dx relies on) and DFT for 16-bit outputs (whose own rounding dominates);
  *        DFT on its other geometries; else STAT where eligible, else MFMA for block_size <= 128,
  *        else VALU. */
 enum bcfft_algo { BCFFT_ALGO_AUTO = 0, BCFFT_ALGO_MFMA = 1, BCFFT_ALGO_VALU = 2, BCFFT_ALGO_STAT = 3,
-                  BCFFT_ALGO_DFT = 4, BCFFT_ALGO_DFTX = 5 };
+                  BCFFT_ALGO_DFT = 4, BCFFT_ALGO_DFTX = 5, BCFFT_ALGO_DFTP = 6 };
 
 enum bcfft_status {
   BCFFT_OK = 0,

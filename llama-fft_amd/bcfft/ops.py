@@ -75,7 +75,7 @@ def forward_glu(x2d: torch.Tensor, spec_gu: torch.Tensor, block_size: int, gate_
     spectra(glu_weights(c_gate, c_up)). h has x2d's dtype. algo: None -> BCFFT_ALGO env (auto:
     the DFT kernel at b = 128 with K = 4096, else stationary), or "stationary" / "dft" / "dftx"."""
     algo = default_algo() if algo is None else algo
-    if algo not in ("auto", "stationary", "dft", "dftx"):
+    if algo not in ("auto", "stationary", "dft", "dftx", "dftp"):
         raise ValueError(f"bcfft.forward_glu: engine {algo!r} has no fused gate/up form "
                          "(auto, stationary, dft, dftx); run gate and up as two forwards instead")
     _lib.require_device(x2d, "bcfft.forward_glu")
@@ -163,7 +163,7 @@ def glu_eligible(in_features: int, block_size: int, dtype: torch.dtype | None = 
     dm = block_size == 128 and n_in == 32
     dm64 = block_size == 64 and n_in == 64 and dtype == torch.bfloat16
     stat = dm or (block_size == 64 and n_in in (32, 64))
-    if algo == "dftx":
+    if algo in ("dftx", "dftp"):
         return dm
     if algo == "dft":
         return dm or dm64

@@ -76,6 +76,14 @@ __device__ __forceinline__ float load_scalar(const void* p, int64_t i, int dt) {
   uint32_t h = ((const uint16_t*)p)[i];
   return dt == BCFFT_BF16 ? bf16_to_f32(h) : f16_to_f32(h);
 }
+// elements i .. i + 3 (i a multiple of 4; p 16-B aligned) as fp32: one 16-B or 8-B load
+__device__ __forceinline__ float4 load4(const void* p, int64_t i, int dt) {
+  if (dt == BCFFT_F32) return *reinterpret_cast<const float4*>((const float*)p + i);
+  const uint2 w = *reinterpret_cast<const uint2*>((const uint16_t*)p + i);
+  if (dt == BCFFT_BF16)
+    return make_float4(bf16_to_f32(w.x & 0xffffu), bf16_to_f32(w.x >> 16), bf16_to_f32(w.y & 0xffffu), bf16_to_f32(w.y >> 16));
+  return make_float4(f16_to_f32(w.x & 0xffffu), f16_to_f32(w.x >> 16), f16_to_f32(w.y & 0xffffu), f16_to_f32(w.y >> 16));
+}
 // v = hi + lo with hi, lo bf16 (hardware RNE, one v_cvt_pk_bf16_f32 per pair): returns packed
 // (lo16 = first, hi16 = second) pairs
 __device__ __forceinline__ void split_bf16(float2 v, uint32_t& hi, uint32_t& lo) {
@@ -486,7 +494,8 @@ inline int64_t group_grid(int64_t cus, int groups, int64_t n_mtiles) {
 // every output block keeps fp16's full range, however quiet it is next to the others (one global
 // scale pushed the per-bin products of a 1e-4-quiet block into fp16 subnormals).
 struct SpecLayout {
-  int64_t packed_f2, tw_off_f2, img_off_u32, img_u32, stat_off_u32, stat_u32, osc_off_u32, total_bytes;
+  int64_t packed_f2, tw_off_f2, img_off_u32, img_u32, stat_off_u32, stat_u32, osc_off_u32, lo8_off_u32, lo8_u32,
+      total_bytes;
   int n_chunk, n_out_pad, stat_groups, stat_pieces;
 };
 int device_cu_count();         // CUs of the current device (bcfft_stat.hip)
@@ -546,7 +555,12 @@ __host__ __device__ inline SpecLayout spec_layout(int n_out, int n_in, int b) {
   }
   s.osc_off_u32 = s.stat_off_u32 + s.stat_u32;         // per-output-block inverse scales
   s.stat_u32 += (int64_t)s.stat_groups * STAT_OUT_BLOCKS;
-  s.total_bytes = (s.stat_off_u32 + s.stat_u32) * 4;
+  // the precise engine's weight residual (bcfft_dm.hip, EP): b = 128, K = 4096 only. Per output
+  // group, per wave (8), per bin of the wave (8), per K-step (2), per lane: 16 B = the e4m3 of
+  // conj(C) s_o - fp16(conj(C) s_o) for the lane's 8 B-fragment elements of N-tile 0, then N-tile 1
+  s.lo8_off_u32 = s.stat_off_u32 + s.stat_u32;
+  s.lo8_u32 = (b == 128 && n_in == 32) ? (int64_t)s.stat_groups * 8 * 8 * 2 * 64 * 4 : 0;
+  s.total_bytes = (s.lo8_off_u32 + s.lo8_u32) * 4;
   return s;
 }
 
@@ -559,11 +573,13 @@ bool launch_forward_stat(int b, int n_in, int xdt, bool yf32, const void* x, int
 bool launch_forward_glu(int b, int n_in, int xdt, const void* x, int64_t n, int n_gate, const void* spec,
                         void* h, hipStream_t s);
 void launch_stat_image(int b, int n_out, int n_in, void* spec, hipStream_t s);
+// the precise engine's e4m3 weight residual image (b = 128, K = 4096; after launch_stat_image)
+void launch_lo8_image(int n_out, void* spec, hipStream_t s);
 // DFT-on-MFMA kernel (bcfft_dm.hip): the STAT image's geometry subset b = 128, K = 4096
 bool dm_eligible(int n_in, int b);
-bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, bool exact, const void* x, int64_t n, int n_out,
+bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, int mode, const void* x, int64_t n, int n_out,
                        const void* spec, const void* bias, int bias_dt, void* y, hipStream_t s);
-bool launch_forward_dm_glu(int b, int n_in, int xdt, bool exact, const void* x, int64_t n, int n_gate,
+bool launch_forward_dm_glu(int b, int n_in, int xdt, int mode, const void* x, int64_t n, int n_gate,
                            const void* spec, void* h, hipStream_t s);
 bool dm8_eligible(int n_in, int b, int xdt, bool yf32);
 // several output groups at bf16 I/O (bcfft_dmg.hip): one workgroup runs a token tile's stage 1

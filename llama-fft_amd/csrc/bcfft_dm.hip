@@ -47,6 +47,12 @@ constexpr int SC_OFF = F_OFF + 16384;               // scale exponents [2 parity
 constexpr int OS_OFF = SC_OFF + 64;                  // the group's 32 inverse weight scales
 constexpr int LDS_BYTES = OS_OFF + 128;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+// precise engine (EP): the e4m3 table residual, pair-packed (rows 2p, 2p + 1 of a column in one
+// 16-bit element), 32 pair-rows at a 288-B stride (a 32-lane half's 8 pair-rows fall on distinct
+// 8-bank groups for both the stage-1 transposed reads and the stage-3 16-B row reads)
+constexpr int FL_OFF = LDS_BYTES, FL_STRIDE = 288;
+constexpr int LDS_BYTES_EP = FL_OFF + 32 * FL_STRIDE;
+static_assert(LDS_BYTES_EP <= 160 * 1024, "LDS budget (EP)");
 
 // X unit (16 B = 4 input blocks x (re, im) fp16 of bin f, precision p, block quad q) of the
 // token in slot tok, K-step ks; swizzle: the precision bit flips with bin bit 2, the quad with
@@ -60,11 +66,40 @@ __device__ __forceinline__ int yunit(int w, int o, int par) { return w * 1024 + 
 
 }  // namespace dmk
 
-template <int XT, bool YF32, bool EX, bool GLU>
-__global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
+// bf8 (e5m2) of eight fp16 values: the high byte of each (fp16 and e5m2 share sign and exponent
+// fields, so this is the value truncated to 2 mantissa bits). (w0, w1, w2, w3) hold the values in
+// order, two per word; the result keeps that order, one byte each (an fp8 MFMA operand).
+__device__ __forceinline__ long bf8x8(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  const uint32_t lo = __builtin_amdgcn_perm(w1, w0, 0x07050301u), hi = __builtin_amdgcn_perm(w3, w2, 0x07050301u);
+  return (long)(((uint64_t)hi << 32) | lo);
+}
+
+// EP (precise engine, BCFFT_ALGO_DFTP; bit 1: stage-1 table residual, 2: weight residual, 4:
+// stage-3 table residual; 0 = the dft / dftx kernel): every fp16 single term of the dftx kernel
+// gets its rounding residual back through an fp8 MFMA into the same fp32 accumulator:
+//   * the table is F 2^8 in fp16 (kDmFp) and a is scaled 2^15 lower, so D's scale is unchanged;
+//     the residual F 2^8 - kDmFp (|.| <= 2^-3) is e4m3 (kDmFl8) and multiplies a bf8 copy of the
+//     data's fp16 hi term (the high byte: same value range), in the same fp32 accumulator;
+//   * stage 2 adds A(bf8) x e4m3(conj(C) s_o - fp16(conj(C) s_o)) (the lo8 image, streamed from L2
+//     by every wave for its bins, four bins ahead) to the fp16 product's accumulator;
+//   * stage 3 adds e4m3 table residual x bf8(Y hi).
+// The x DMA is issued by the I waves at the end of P1, so an F wave issues no asm VMEM operation
+// and the compiler's counted waits on its lo8 loads are exact. Numpy mirror: tests/dm_model.py
+// (precise=True); error ~1e-5 relative (north star 1e-3), per token ~1e-5 x its cancellation.
+#ifndef BCFFT_DM_LB
+#define BCFFT_DM_LB 2
+#endif
+// BM: bias handling, -1 = by the runtime bias_dt (dft / dftx); 0 = none, 1 = fp32 bias, 2 = 16-bit
+// bias, its 4 consecutive values per lane read by one buffer load (the precise engine: the general
+// per-element path's address registers do not fit beside its residual operands)
+template <int XT, bool YF32, bool EX, bool GLU, int EP = 0, int BM = -1>
+__global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_out, const uint32_t* __restrict__ stat,
-    const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
+    const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv,
+    const uint4* __restrict__ lo8) {
   using namespace dmk;
+  static_assert(EP == 0 || EX, "the precise engine extends the exact (hi + lo) variant");
+  constexpr bool DMA_P1 = false;                    // (experiment switch: I waves issue the next x at the end of P1)
   constexpr int ES = XTraits<XT>::ES;
   constexpr bool Y32 = YF32 || XT == BCFFT_F32;
   constexpr int ESY = Y32 ? 4 : 2;
@@ -78,7 +113,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
 #else
 #define SUBSTAMP(id) do { if (sub_on) STAMP(id); } while (0)
 #endif
-  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  __shared__ __attribute__((aligned(16))) char lds[EP ? LDS_BYTES_EP : LDS_BYTES];
   int* wsc = reinterpret_cast<int*>(lds + SC_OFF);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -141,12 +176,16 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
   // ---- prologue: first tile's x (I waves), the DFT table, the stationary B fragments
   if (fwave && wg_in_grp < n_mtiles) dma_token(wg_in_grp, lds, 0, NDMA);
   {
-    const uint4* tab = reinterpret_cast<const uint4*>(kDmF);
+    const uint4* tab = reinterpret_cast<const uint4*>(EP ? kDmFp : kDmF);
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int c = tid + 512 * r;                  // chunk c: row c >> 4, chunk c & 15
       const int t = c >> 4, ch = c & 15;
       *reinterpret_cast<uint4*>(lds + F_OFF + 256 * t + 16 * (ch ^ fsw(t))) = tab[c];
+    }
+    if constexpr (EP != 0) {                        // residual image: pair-row tid >> 4, 16-B piece tid & 15
+      *reinterpret_cast<uint4*>(lds + FL_OFF + FL_STRIDE * (tid >> 4) + 16 * (tid & 15)) =
+          reinterpret_cast<const uint4*>(kDmFl8)[tid];
     }
   }
   f16x8 creg[BW][KS][NT];
@@ -193,6 +232,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     const int q4 = (l & 15) >> 2, p4 = l & 3;
     const int cx = (p4 >> 1) ^ fsw(8 * g + q4);
     const int trb = F_OFF + 256 * (8 * g + q4) + 8 * (p4 & 1);
+    // EP: residual A fragments, one transposed read each: lane 4 q4 + p4 of group g supplies
+    // pair-row 4 g + q4 (t = 8 g + 2 q4, + 1), columns 4 p4 .. 4 p4 + 3 of the tile's 16
+    const int flb = FL_OFF + FL_STRIDE * (4 * g + q4) + 8 * p4;
     // X write lane bases: precision p at (4 (p ^ (g & 1)) + (q ^ phi)) units
     const int xq = (b16 >> 2) ^ (3 * (wave >> 1));
     const int xw0 = 128 * 4 * g + 16 * (4 * (g & 1) + xq) + 4 * (b16 & 3);
@@ -242,7 +284,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
       // across lanes as magnitude bits: no NaN canonicalisation around the DPP moves
       const int sx = stat_scale_exp(2.f * __uint_as_float(wave_umax(__float_as_uint(mxf))));   // |a|, |d| <= 2 max|x|
       if (l == 0) wsc[par * 8 + wave * 2 + h] = sx - 7;     // X = D 2^-(sx - 7): the table's 2^-7
-      const float S = __int_as_float((sx + 127) << 23);
+      // EP: a 2^(sx - 15) against the table 2^8 (the same D); max|x| < 2^125 keeps the scale normal
+      const float S = __int_as_float((EP ? max(sx - 15, -126) + 127 : sx + 127) << 23);
       SUBSTAMP(56 + 4 * hh);
       f32x4 acc[8];
 #pragma unroll
@@ -266,6 +309,23 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
           }
         }
         const f16x8 bah = frag(ah[0], ah[1], ah[2], ah[3]), bdh = frag(dh[0], dh[1], dh[2], dh[3]);
+        long b8a = 0, b8d = 0;
+        if constexpr ((EP & 1) != 0) {
+          b8a = bf8x8(ah[0], ah[1], ah[2], ah[3]);
+          b8d = bf8x8(dh[0], dh[1], dh[2], dh[3]);
+        }
+        // EP: the K-step's eight residual A fragments, read before its MFMAs. (Read in between,
+        // hipcc gave a read the registers of an operand that an issued, still queued MFMA had
+        // not consumed yet (no wait for it on gfx950): garbage in the accumulators. Hoisted,
+        // they land in registers of their own.)
+        s16x4 rlv[8];
+        if constexpr ((EP & 1) != 0) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            rlv[i] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) s16x4*)(lds + flb + FL_STRIDE * 16 * ks + 32 * i));
+          __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int pr = 0; pr < 2; ++pr)
 #pragma unroll
@@ -280,6 +340,11 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
             if constexpr (EX) {
               const f16x8 bal = frag(al[0], al[1], al[2], al[3]), bdl = frag(dl[0], dl[1], dl[2], dl[3]);
               acc[4 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, pr ? bdl : bal, acc[4 * pr + mt], 0, 0, 0);
+            }
+            if constexpr ((EP & 1) != 0) {          // + e4m3 table residual x bf8(hi), pair-rows 16 ks + 4 g + q
+              const s16x4 rl = rlv[4 * pr + mt];
+              acc[4 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_bf8(__builtin_bit_cast(long, rl), pr ? b8d : b8a,
+                                                                           acc[4 * pr + mt], 0, 0, 0);
             }
           }
       }
@@ -304,11 +369,32 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     }
   };
 
+  // ---- EP: the wave's lo8 fragments (16 B per (bin, K-step): N-tile 0 then 1), a ring of four
+  // bins: bins 0-3 are loaded at the end of P1, bin fb + 4 while stage 2 works on bin fb
+  // (the ring is a per-iteration array handed to stage 2 / stage 3, so that it is dead outside P1's
+  // end .. stage 2 and holds no registers through stage 1)
+  // one buffer descriptor per wave over its 16 KiB of fragments: lane offset in one VGPR, the
+  // (bin, K-step) piece in the scalar offset
+  const __amdgpu_buffer_rsrc_t clrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint4*>(lo8) + ((EP & 2) ? (int64_t)(grp_o * NW + wave) * BW * KS * 64 : 0), 0,
+      (EP & 2) ? BW * KS * 1024 : 0, 0x00020000);
+#ifndef BCFFT_DFTP_RING
+#define BCFFT_DFTP_RING 4
+#endif
+  constexpr int RING = BCFFT_DFTP_RING;             // bins of lo8 fragments in flight
+  typedef u32x4 ClRing[RING][KS];
+  auto cl_load = [&](ClRing& clr, int fb) {
+    asm volatile("" ::: "memory");                  // keep the loads here: hoisted, they would hold
+#pragma unroll                                      // their registers through the phase before
+    for (int ks = 0; ks < KS; ++ks)
+      clr[fb % RING][ks] = __builtin_amdgcn_raw_buffer_load_b128(clrs, 16 * opaque(lane), (fb * KS + ks) * 1024, 0);
+  };
+
   // ---- stage 2 (all waves): per-bin complex MAC on bins f = 8 wave + fb; Y units over the
   // wave's own K-step-0 X units (the wave's DS operations execute in order)
   // dma_next: this F wave streams the next tile's x into its slot of `dregion`, a piece or two
   // per bin (spreads the x traffic over the phase instead of one burst at its start)
-  auto stage2 = [&](char* region, int par, bool dma_next, int64_t mnext, char* dregion) {
+  auto stage2 = [&](char* region, int par, bool dma_next, int64_t mnext, char* dregion, ClRing& clr) {
 #if defined(BCFFT_DM_MEMONLY) || (defined(BCFFT_DM_ABL) && (BCFFT_DM_ABL & 2))
     if (dma_next) dma_token(mnext, dregion, 0, NDMA);
     return;
@@ -336,23 +422,31 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     const int xq = kb ^ (3 * (a_t >> 1));
     const char* ab0 = region + a_t * SLOT + wave * 1024 + 16 * (4 * a_prec + xq);        // bins fb < 4
     const char* ab1 = region + a_t * SLOT + wave * 1024 + 16 * (4 * (a_prec ^ 1) + xq);  // fb >= 4
-    uint4 araw[BW][KS];
-#pragma unroll
-    for (int fb = 0; fb < BW; ++fb)
+    // A units: all bins up front (dft / dftx); EP loads each bin's as it goes (its registers
+    // hold the lo8 ring instead)
+    constexpr int NAR = EP ? 1 : BW;
+    uint4 araw[NAR][KS];
+    auto a_load = [&](int fb) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
-        araw[fb][ks] = *reinterpret_cast<const uint4*>((fb < 4 ? ab0 : ab1) + 128 * fb + 8192 * ks);
+        araw[fb % NAR][ks] = *reinterpret_cast<const uint4*>((fb < 4 ? ab0 : ab1) + 128 * fb + 8192 * ks);
+    };
+    if constexpr (!EP) {
+#pragma unroll
+      for (int fb = 0; fb < BW; ++fb) a_load(fb);
+    }
     uint32_t yh[BW][NT], yl[BW][NT];
 #pragma unroll
     for (int fb = 0; fb < BW; ++fb) {
       const int f = wave * BW + fb;
       if (dma_next) dma_token(mnext, dregion, fb * (NDMA / BW), (fb + 1) * (NDMA / BW));
+      if constexpr (EP != 0) a_load(fb);
       f32x4 acc[NT];
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        uint4 raw = araw[fb][ks];
+        uint4 raw = araw[fb % NAR][ks];
         if (f == 0) {
           raw.x = pkmul(raw.x, amul0[ks]); raw.y = pkmul(raw.y, amul0[ks]);
           raw.z = pkmul(raw.z, amul0[ks]); raw.w = pkmul(raw.w, amul0[ks]);
@@ -366,6 +460,12 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
           acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, creg[fb][ks][nt], acc[nt], 0, 0, 0);
+        if constexpr ((EP & 2) != 0) {              // + bf8(A) x e4m3 weight residual, same accumulators
+          const long a8 = bf8x8(raw.x, raw.y, raw.z, raw.w);
+          const u32x4 c8 = clr[fb % RING][ks];
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf8_fp8(a8, (long)(((uint64_t)c8.y << 32) | c8.x), acc[0], 0, 0, 0);
+          acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf8_fp8(a8, (long)(((uint64_t)c8.w << 32) | c8.z), acc[1], 0, 0, 0);
+        }
       }
       constexpr float YS = 1.f / 2097152.f;          // 2^-21: |Y| < 2^14 in fp16
 #pragma unroll
@@ -374,6 +474,16 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
         const float yr = (acc[nt][0] + acc[nt][1]) * YS, yi = (acc[nt][2] + acc[nt][3]) * YS;
         if constexpr (EX) split2(yr, yi, yh[fb][nt], yl[fb][nt]);
         else yh[fb][nt] = pk_rne(yr, yi);
+      }
+      // EP: refill the ring slot only now that the bin's accumulators have been read, i.e. its
+      // MFMAs have finished with the slot's registers (a load issued right after them can
+      // overwrite an operand a queued MFMA has not read yet, as in stage 1)
+      if constexpr ((EP & 2) != 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (fb + RING < BW) cl_load(clr, fb + RING);
+#ifndef BCFFT_DFTP_NO_SCHED_BARRIER
+        __builtin_amdgcn_sched_barrier(0);          // one bin at a time: the overlapped schedule spills
+#endif
       }
     }
     char* yb = region + yt * SLOT + wave * 1024 + 16 * (ml & 15);
@@ -398,9 +508,14 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     char* slot = region + tslot * SLOT;
     const int* sc = wsc + par * 8 + tslot * 2;
     const int nmin = min(sc[0], sc[1]);
-    float ysc[NT];                                  // output block o = 16 nt + o16: 1 / s_o
+    float ysc[NT];                                  // output block o = 16 nt + o16: 1 / s_o (EP: the table's 2^8)
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) ysc[nt] = __builtin_ldexpf(reinterpret_cast<const float*>(lds + OS_OFF)[16 * nt + o16], 30 - nmin);
+    for (int nt = 0; nt < NT; ++nt)
+      ysc[nt] = __builtin_ldexpf(reinterpret_cast<const float*>(lds + OS_OFF)[16 * nt + o16], (EP ? 15 : 30) - nmin);
+    // EP: residual A fragments of table row t = 16 mt + o16: the 16-B pairs of columns
+    // 64 pr + 32 ks + 8 g .. + 7 in pair-row t >> 1, the byte of row parity t & 1 picked by perm
+    const int fl3 = FL_OFF + FL_STRIDE * (o16 >> 1) + 16 * g;
+    const uint32_t flsel = (o16 & 1) ? 0x07050301u : 0x06040200u;
     // all Y fragments of the token: B[k = 8 g + j][o] = unit(wave 4 ks + g, o, parity)
     constexpr int NYP = EX ? 2 : 1;                 // Y precision terms (hi; lo 8 KiB further)
     constexpr bool YSP_PREF_OFF = EX;               // the lo terms take the table prefetch's VGPRs
@@ -466,6 +581,23 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
             E[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][0], __builtin_bit_cast(f16x8, yf[yp][ks][0][nt]), E[nt], 0, 0, 0);
             O[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][1], __builtin_bit_cast(f16x8, yf[yp][ks][1][nt]), O[nt], 0, 0, 0);
           }
+      if constexpr ((EP & 4) != 0) {                // + e4m3 table residual x bf8(Y hi)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+          for (int pr = 0; pr < 2; ++pr) {
+            asm volatile("" ::: "memory");          // one residual fragment at a time (registers)
+            const uint4 w = *reinterpret_cast<const uint4*>(lds + fl3 + 2304 * mt + 128 * pr + 64 * ks);
+            const long fl = (long)(((uint64_t)__builtin_amdgcn_perm(w.w, w.z, flsel) << 32) |
+                                   __builtin_amdgcn_perm(w.y, w.x, flsel));
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+              const uint4 v = yf[0][ks][pr][nt];
+              f32x4& acc3 = pr ? O[nt] : E[nt];
+              acc3 = __builtin_amdgcn_mfma_f32_16x16x32_fp8_bf8(fl, bf8x8(v.x, v.y, v.z, v.w), acc3, 0, 0, 0);
+            }
+          }
+      }
       // rows t = 16 mt + 4 g + r (and t + 64), column o = 16 nt + o16
       if constexpr (GLU) {                          // h = silu(gate) * up of block o16
         float gu[NT][2][4];
@@ -502,10 +634,13 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = hf ? fmaf(E[nt][r], ysc[nt], -os[r]) : fmaf(E[nt][r], ysc[nt], os[r]);
-          if (Y32 || bias_dt != BCFFT_NONE) {       // .to(x dtype) :266, + bias :270-271
+          // the precise engine (BM >= 0, fp32 outputs) adds its bias to the staged rows at the store
+          // phase instead (the same value: v is already in its fp32 form), where registers are free
+          const bool has_bias = BM < 0 && bias_dt != BCFFT_NONE;
+          if (Y32 || has_bias) {                    // .to(x dtype) :266, + bias :270-271
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = round_to(v[r], XT);
-            if (bias_dt != BCFFT_NONE && o < nvalid) {
+            if (has_bias && o < nvalid) {
               const int64_t cc = (int64_t)(grp_o * NOG + o) * B + 16 * mt + 4 * g + 64 * hf;
 #pragma unroll
               for (int r = 0; r < 4; ++r) v[r] += load_scalar(bias, cc + r, bias_dt);
@@ -520,6 +655,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
           }
         }
       }
+      if constexpr ((EP & 4) != 0) __builtin_amdgcn_sched_barrier(0);   // one mt at a time (registers)
       if (mt < 3) {
         if (YSP_PREF_OFF) {
           gload(mt + 1, gcur);                      // no prefetch: registers for the Y lo terms
@@ -542,6 +678,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
         (char*)yv + (tok_ok ? tok : 0) * M * ESY + (int64_t)grp_o * OPG * RB, 0,
         tok_ok ? (int)((M - (int64_t)grp_o * OPG * B) * ESY) : 0, 0x00020000);
     constexpr int NQ = GLU && !Y32 ? 4 : 8;         // store instructions per half (GLU 16-bit: 16 rows)
+
     const int vofs = lr * RB + 16 * w;
     // LDS read bases: fp32 row s16 = 2 q + lr, unit w ^ (s16 & 7) = (w ^ lr) ^ 2 (q & 3);
     // 16-bit row rr = 4 q + lr, unit w ^ (rr & 7) = (w ^ lr) ^ 4 (q & 1)
@@ -556,6 +693,27 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
       for (int q = 0; q < NQ; ++q) {
         if constexpr (Y32) {                        // rows 16 half + 2 q + lr: N-tile half's staging
           d[q] = *reinterpret_cast<const uint4*>(slot + (half ? 0 : 8192) + 1024 * q + rdb[q & 3]);
+          if constexpr (BM >= 1) {                  // + bias of output row 16 half + 2 q + lr, t = 4 w .. 4 w + 3
+            static_assert(!GLU, "no bias on the fused gate/up");
+            const int bes = BM == 1 ? 4 : 2;
+            const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<char*>((const char*)bias) + (int64_t)grp_o * NOG * B * bes, 0,
+                (int)((M - (int64_t)grp_o * NOG * B) * bes), 0x00020000);
+            const int boff = (lr * B + 4 * w) * bes, bimm = ((16 * half + 2 * q) * B) * bes;
+            float4 bv;
+            if constexpr (BM == 1) {
+              bv = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(brs, boff, bimm, 0));
+            } else {
+              const u32x2 bw = __builtin_amdgcn_raw_buffer_load_b64(brs, boff, bimm, 0);
+              bv = bias_dt == BCFFT_BF16
+                       ? make_float4(bf16_to_f32(bw.x & 0xffffu), bf16_to_f32(bw.x >> 16), bf16_to_f32(bw.y & 0xffffu),
+                                     bf16_to_f32(bw.y >> 16))
+                       : make_float4(f16_to_f32(bw.x & 0xffffu), f16_to_f32(bw.x >> 16), f16_to_f32(bw.y & 0xffffu),
+                                     f16_to_f32(bw.y >> 16));
+            }
+            d[q] = make_uint4(__float_as_uint(__uint_as_float(d[q].x) + bv.x), __float_as_uint(__uint_as_float(d[q].y) + bv.y),
+                              __float_as_uint(__uint_as_float(d[q].z) + bv.z), __float_as_uint(__uint_as_float(d[q].w) + bv.w));
+          }
         } else {
           uint4 v = *reinterpret_cast<const uint4*>(slot + 8192 + 1024 * q + rdb[q & 1]);
           if (q & 2) v = make_uint4(v.z, v.w, v.x, v.y);   // rows with bit 3: 8-B halves swapped
@@ -599,14 +757,29 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
       stage3(other, par ^ 1, m - gstride);
     }
 #if defined(BCFFT_DM_DMAP1)
-    if (!fwave && m + gstride < n_mtiles) {
+    constexpr bool dma_p1 = true;
+#else
+    constexpr bool dma_p1 = DMA_P1;
+#endif
+    if (dma_p1 && !fwave && m + gstride < n_mtiles) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       dma_token(m + gstride, other, 0, NDMA);
     }
-#endif
     STAMP(sb + 1);
     if (!have_f) break;
+    // EP: the first lo8 bins of stage 2, issued by every wave here (one definition point: the
+    // ring holds no registers through stage 1 or stage 3) and waited for after Ba, before the F
+    // waves' x DMA: the compiler counts none of the asm DMA, so a wait behind it would drain it
+    ClRing clr;
+    if constexpr ((EP & 2) != 0) {
+#pragma unroll
+      for (int i = 0; i < RING; ++i) cl_load(clr, i);
+    }
     lds_barrier();                                  // Ba: X units and scales complete
+    if constexpr ((EP & 2) != 0) {
+#pragma unroll
+      for (int i = 0; i < RING; ++i) asm volatile("" : "+v"(clr[i][0]), "+v"(clr[i][1]));
+    }
     STAMP(sb + 2);
     // F wave j streams the next tile's x for its slot j of the other region: stage 3 has read
     // that slot's Y and staged y (each wave's LDS reads completed before Ba)
@@ -618,13 +791,15 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
 #elif defined(BCFFT_DM_DMAINTER)                    // experiment: pieces between the stage-2 bins
     const bool dma2 = fwave && m + gstride < n_mtiles;
 #else                                               // one burst at the start of phase 2 (measured best)
-    if (fwave && m + gstride < n_mtiles) dma_token(m + gstride, other, 0, NDMA);
+    if (!DMA_P1 && fwave && m + gstride < n_mtiles) dma_token(m + gstride, other, 0, NDMA);
     const bool dma2 = false;
 #endif
     STAMP(sb + 3);
-    stage2(region, par, dma2, m + gstride, other);
+    stage2(region, par, dma2, m + gstride, other, clr);
 #if defined(BCFFT_DM_DMASPLIT) || defined(BCFFT_DM_DMAP1)
     if (!fwave) wait_vmcnt<0>();                    // their share of the next x has landed
+#else
+    if (DMA_P1 && !fwave) wait_vmcnt<0>();          // EP: the next tile's x (issued by this I wave) has landed
 #endif
     STAMP(sb + 4);
     lds_barrier();                                  // Bb: Y units complete
@@ -636,7 +811,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
 }  // namespace bcfft
 
 namespace {
-template <int XT, bool YF32, bool EX, bool GLU = false>
+#ifndef BCFFT_DFTP_EP
+#define BCFFT_DFTP_EP 7                             // analysis builds: which residual terms the precise engine adds
+#endif
+template <int XT, bool YF32, bool EX, bool GLU = false, int EP = 0, int BM = -1>
 void launch_dm(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt, void* y,
                hipStream_t s) {
   const int groups = GLU ? (n_out + 15) / 16 : (n_out + 31) / 32;
@@ -645,8 +823,9 @@ void launch_dm(const void* x, int64_t n, int n_out, const void* spec, const void
   const int64_t total = bcfft::group_grid(bcfft::device_cu_count(), groups, n_mtiles);
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
   const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
-  hipLaunchKernelGGL((bcfft::bc_forward_dm_kernel<XT, YF32, EX, GLU>), dim3((unsigned)total), dim3(512), 0, s, x,
-                     n, n_out, stat, osc, bias, bias_dt, y);
+  const uint4* lo8 = reinterpret_cast<const uint4*>(reinterpret_cast<const uint32_t*>(spec) + sl.lo8_off_u32);
+  hipLaunchKernelGGL((bcfft::bc_forward_dm_kernel<XT, YF32, EX, GLU, EP, BM>), dim3((unsigned)total), dim3(512), 0, s, x,
+                     n, n_out, stat, osc, bias, bias_dt, y, lo8);
 }
 }  // namespace
 
@@ -665,13 +844,37 @@ extern "C" int bcfft_set_stamps_dm(void* buf) {
 namespace bcfft {
 bool dm_eligible(int n_in, int b) { return b == 128 && n_in == 32; }
 
-// exact: Y as hi + lo (BCFFT_ALGO_DFTX); fp16 outputs always take it
-bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, bool exact, const void* x, int64_t n, int n_out,
+// mode 0: dft; 1 (exact): Y as hi + lo (BCFFT_ALGO_DFTX), which fp16 outputs always take; 2: the
+// precise engine (BCFFT_ALGO_DFTP) for fp32 outputs (16-bit outputs: DFTX, whose error already sits
+// far below their rounding)
+bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, int mode, const void* x, int64_t n, int n_out,
                        const void* spec, const void* bias, int bias_dt, void* y, hipStream_t s) {
   if (!dm_eligible(n_in, b)) return false;
-#define BCFFT_DM_LAUNCH(XT, YF)                                                      \
-  (exact ? launch_dm<XT, YF, true>(x, n, n_out, spec, bias, bias_dt, y, s)          \
-         : launch_dm<XT, YF, false>(x, n, n_out, spec, bias, bias_dt, y, s))
+  const bool exact = mode >= 1;
+  if (mode == 2 && yf32) {
+    constexpr int P = BCFFT_DFTP_EP;
+    const int bm = bias_dt == BCFFT_NONE ? 0 : bias_dt == BCFFT_F32 ? 1 : 2;
+#define BCFFT_DMP_LAUNCH(XT)                                                                              \
+  (bm == 0 ? launch_dm<XT, true, true, false, P, 0>(x, n, n_out, spec, bias, bias_dt, y, s)              \
+   : bm == 1 ? launch_dm<XT, true, true, false, P, 1>(x, n, n_out, spec, bias, bias_dt, y, s)            \
+             : launch_dm<XT, true, true, false, P, 2>(x, n, n_out, spec, bias, bias_dt, y, s))
+    if (xdt == BCFFT_F32) BCFFT_DMP_LAUNCH(BCFFT_F32);
+    else if (xdt == BCFFT_F16) BCFFT_DMP_LAUNCH(BCFFT_F16);
+    else BCFFT_DMP_LAUNCH(BCFFT_BF16);
+#undef BCFFT_DMP_LAUNCH
+    return true;
+  }
+  // fp32 outputs with a bias add it at the store phase (BM = 1 / 2: one buffer load per 4 values);
+  // the per-element path of BM = -1 costs ~50 % at the north star's size
+  const int bm = bias_dt == BCFFT_NONE ? 0 : bias_dt == BCFFT_F32 ? 1 : 2;
+#define BCFFT_DM_LAUNCH_EX(XT, EXV)                                                                       \
+  (!yf32 || bm == 0 ? launch_dm<XT, true, EXV>(x, n, n_out, spec, bias, bias_dt, y, s)                  \
+   : bm == 1        ? launch_dm<XT, true, EXV, false, 0, 1>(x, n, n_out, spec, bias, bias_dt, y, s)     \
+                    : launch_dm<XT, true, EXV, false, 0, 2>(x, n, n_out, spec, bias, bias_dt, y, s))
+#define BCFFT_DM_LAUNCH(XT, YF)                                                                           \
+  (YF ? (exact ? BCFFT_DM_LAUNCH_EX(XT, true) : BCFFT_DM_LAUNCH_EX(XT, false))                             \
+      : (exact ? launch_dm<XT, YF, true>(x, n, n_out, spec, bias, bias_dt, y, s)                          \
+               : launch_dm<XT, YF, false>(x, n, n_out, spec, bias, bias_dt, y, s)))
 #ifndef BCFFT_NO_DM8
   if (!exact && dm8_eligible(n_in, b, xdt, yf32)) {  // bf16 I/O: 8 tokens per tile
 #ifndef BCFFT_NO_DMG
@@ -690,13 +893,19 @@ bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, bool exact, const vo
   else if (yf32) BCFFT_DM_LAUNCH(BCFFT_BF16, true);
   else BCFFT_DM_LAUNCH(BCFFT_BF16, false);
 #undef BCFFT_DM_LAUNCH
+#undef BCFFT_DM_LAUNCH_EX
   return true;
 }
 
 // fused gate/up + SwiGLU (bcfft_forward_glu): h has x's dtype, no bias; fp16 takes the exact variant
-bool launch_forward_dm_glu(int b, int n_in, int xdt, bool exact, const void* x, int64_t n, int n_gate,
+bool launch_forward_dm_glu(int b, int n_in, int xdt, int mode, const void* x, int64_t n, int n_gate,
                            const void* spec, void* h, hipStream_t s) {
   if (!dm_eligible(n_in, b)) return false;
+  const bool exact = mode >= 1;
+  if (mode == 2 && xdt == BCFFT_F32) {             // precise engine: fp32 h only (16-bit h: DFTX)
+    launch_dm<BCFFT_F32, true, true, true, BCFFT_DFTP_EP, 0>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
+    return true;
+  }
   if (xdt == BCFFT_F32) {
     if (exact) launch_dm<BCFFT_F32, true, true, true>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
     else launch_dm<BCFFT_F32, true, false, true>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);

@@ -592,6 +592,7 @@ const char* algo_name(int a) {
     case BCFFT_ALGO_STAT: return "stationary";
     case BCFFT_ALGO_DFT: return "dft";
     case BCFFT_ALGO_DFTX: return "dftx";
+    case BCFFT_ALGO_DFTP: return "dftp";
     default: return "?";
   }
 }
@@ -710,6 +711,7 @@ void launch_spectra(const void* c, int c_dt, int n_out, int n_in, int tc, float2
     hipLaunchKernelGGL(bcfft::bc_mfma_image_kernel<B>, dim3(blocks), dim3(256), 0, s, n_out, n_in, out);
   }
   bcfft::launch_stat_image(B, n_out, n_in, out, s);   // no-op unless stat_eligible
+  if (B == 128 && n_in == 32) bcfft::launch_lo8_image(n_out, out, s);   // the precise engine's residual
 }
 }  // namespace
 
@@ -793,7 +795,7 @@ static int64_t ws_bytes_for(int64_t n_tokens, int in_features, int out_features,
     const int kz = bcfft::dmk_ksplit(n_tokens, in_features / block_size, out_features / block_size);
     return kz < 2 ? 0 : kz * n_tokens * (int64_t)out_features * (int64_t)sizeof(float);
   }
-  if (a == BCFFT_ALGO_DFT || a == BCFFT_ALGO_DFTX || a == BCFFT_ALGO_STAT) return 0;
+  if (a == BCFFT_ALGO_DFT || a == BCFFT_ALGO_DFTX || a == BCFFT_ALGO_DFTP || a == BCFFT_ALGO_STAT) return 0;
   int kz = 1;
   if (a == BCFFT_ALGO_MFMA && block_size <= BCFFT_MFMA_MAXB) kz = mfma_ksplit(n_tokens, n_in, block_size);
   else if (a == BCFFT_ALGO_VALU || a == BCFFT_ALGO_MFMA) kz = valu_ksplit(n_tokens, n_in, block_size);
@@ -825,9 +827,7 @@ int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_featur
     return BCFFT_ERR_DTYPE;
   if (y_dtype != promote(x_dtype, bias_dtype)) return BCFFT_ERR_DTYPE;
   if ((bias == nullptr) != (bias_dtype == BCFFT_NONE)) return BCFFT_ERR_ARG;
-  if (algo != BCFFT_ALGO_AUTO && algo != BCFFT_ALGO_MFMA && algo != BCFFT_ALGO_VALU &&
-      algo != BCFFT_ALGO_STAT && algo != BCFFT_ALGO_DFT && algo != BCFFT_ALGO_DFTX)
-    return BCFFT_ERR_ARG;
+  if (algo < BCFFT_ALGO_AUTO || algo > BCFFT_ALGO_DFTP) return BCFFT_ERR_ARG;
   if (n_tokens == 0) return BCFFT_OK;
   if (!x || !y || !spectra) return BCFFT_ERR_ARG;
   if (!aligned16(x) || !aligned16(y) || !aligned16(spectra) || (bias && !aligned16(bias)) ||
@@ -837,7 +837,7 @@ int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_featur
   const bool stat_ok = bcfft::stat_eligible(n_in, block_size);
   if (algo == BCFFT_ALGO_STAT && !stat_ok) return refuse("bcfft_forward", algo, n_in, block_size, x_dtype, y_dtype);
   const bool dm64 = bcfft::dm64_eligible(n_in, block_size, x_dtype, y_dtype == BCFFT_F32);
-  if (algo == BCFFT_ALGO_DFTX && !bcfft::dm_eligible(n_in, block_size))
+  if ((algo == BCFFT_ALGO_DFTX || algo == BCFFT_ALGO_DFTP) && !bcfft::dm_eligible(n_in, block_size))
     return refuse("bcfft_forward", algo, n_in, block_size, x_dtype, y_dtype);
   const bool dmk = bcfft::dmk_eligible(n_in, block_size, x_dtype, y_dtype == BCFFT_F32);
   const bool dm256 = bcfft::dm256_eligible(n_in, block_size, x_dtype, y_dtype == BCFFT_F32);
@@ -868,8 +868,9 @@ int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_featur
     bcfft::launch_forward_dm64(x, n_tokens, n_out, spectra, bias, bias_dtype, y, false, s);
     return record_launch();
   }
-  if (algo == BCFFT_ALGO_DFT || algo == BCFFT_ALGO_DFTX) {
-    bcfft::launch_forward_dm(block_size, n_in, x_dtype, y_dtype == BCFFT_F32, algo == BCFFT_ALGO_DFTX, x, n_tokens,
+  if (algo == BCFFT_ALGO_DFT || algo == BCFFT_ALGO_DFTX || algo == BCFFT_ALGO_DFTP) {
+    bcfft::launch_forward_dm(block_size, n_in, x_dtype, y_dtype == BCFFT_F32,
+                             algo == BCFFT_ALGO_DFTP ? 2 : algo == BCFFT_ALGO_DFTX ? 1 : 0, x, n_tokens,
                              n_out, spectra, bias, bias_dtype, y, s);
     return record_launch();
   }
@@ -897,7 +898,7 @@ static int forward_plan(int64_t n_tokens, int in_features, int out_features, int
       in_features % block_size || out_features % block_size)
     return -1;
   if (!valid_dt(x_dtype) || !valid_dt(y_dtype)) return -1;
-  if (algo < BCFFT_ALGO_AUTO || algo > BCFFT_ALGO_DFTX) return -1;
+  if (algo < BCFFT_ALGO_AUTO || algo > BCFFT_ALGO_DFTP) return -1;
   const int n_in = in_features / block_size, n_out = out_features / block_size;
   const bool yf32 = y_dtype == BCFFT_F32;
   const bool dm = bcfft::dm_eligible(n_in, block_size);
@@ -906,7 +907,7 @@ static int forward_plan(int64_t n_tokens, int in_features, int out_features, int
   const bool dm256 = bcfft::dm256_eligible(n_in, block_size, x_dtype, yf32);
   const bool dm64k = bcfft::dm64k_eligible(n_in, block_size, x_dtype, yf32);
   if (algo == BCFFT_ALGO_STAT && !bcfft::stat_eligible(n_in, block_size)) return -1;
-  if (algo == BCFFT_ALGO_DFTX && !dm) return -1;
+  if ((algo == BCFFT_ALGO_DFTX || algo == BCFFT_ALGO_DFTP) && !dm) return -1;
   if (algo == BCFFT_ALGO_DFT && !dm && !dm64 && !dmk && !dm256 && !dm64k) return -1;
   const int a = resolve_algo(algo, n_in, block_size, x_dtype, yf32, n_tokens);
   if (a == BCFFT_ALGO_DFT && dmk) *kernel = "bc_forward_dmk_kernel";
@@ -918,7 +919,7 @@ static int forward_plan(int64_t n_tokens, int in_features, int out_features, int
   else if (a == BCFFT_ALGO_DFT && bcfft::dm8_eligible(n_in, block_size, x_dtype, yf32))
     *kernel = bcfft::dmg_eligible(n_in, block_size, x_dtype, yf32, n_out, false) && bcfft::multigroup_pays(n_tokens, 3)
                   ? "bc_forward_dmg_kernel" : "bc_forward_dm8_kernel";
-  else if (a == BCFFT_ALGO_DFT || a == BCFFT_ALGO_DFTX) *kernel = "bc_forward_dm_kernel";
+  else if (a == BCFFT_ALGO_DFT || a == BCFFT_ALGO_DFTX || a == BCFFT_ALGO_DFTP) *kernel = "bc_forward_dm_kernel";
   else if (a == BCFFT_ALGO_STAT) *kernel = "bc_forward_stat_kernel";
   else if (a == BCFFT_ALGO_MFMA && block_size <= BCFFT_MFMA_MAXB) *kernel = "bc_forward_mfma_kernel";
   else *kernel = "bc_forward_valu_kernel";
@@ -948,7 +949,8 @@ int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_feat
 int bcfft_forward_glu_algo(const void* x, int x_dtype, int64_t n_tokens, int in_features, int gate_features,
                            int block_size, const void* spectra_gu, void* h, int algo, void* stream) {
   g_last_detail[0] = 0;
-  if (algo != BCFFT_ALGO_AUTO && algo != BCFFT_ALGO_STAT && algo != BCFFT_ALGO_DFT && algo != BCFFT_ALGO_DFTX)
+  if (algo != BCFFT_ALGO_AUTO && algo != BCFFT_ALGO_STAT && algo != BCFFT_ALGO_DFT && algo != BCFFT_ALGO_DFTX &&
+      algo != BCFFT_ALGO_DFTP)
     return BCFFT_ERR_ARG;
   if (!valid_block(block_size)) return refuse("bcfft_forward_glu", algo, 0, block_size, x_dtype, x_dtype);
   if (n_tokens < 0 || in_features <= 0 || gate_features <= 0 || in_features % block_size ||
@@ -973,7 +975,8 @@ int bcfft_forward_glu_algo(const void* x, int x_dtype, int64_t n_tokens, int in_
   // AUTO: fp32 h takes the hi + lo products (DFTX), as bcfft_forward does for fp32 outputs
   if (algo == BCFFT_ALGO_AUTO)
     algo = dm ? (x_dtype == BCFFT_F32 ? BCFFT_ALGO_DFTX : BCFFT_ALGO_DFT) : dm64 ? BCFFT_ALGO_DFT : BCFFT_ALGO_STAT;
-  if (algo == BCFFT_ALGO_DFTX && !dm) return refuse("bcfft_forward_glu", algo, n_in, block_size, x_dtype, x_dtype);
+  if ((algo == BCFFT_ALGO_DFTX || algo == BCFFT_ALGO_DFTP) && !dm)
+    return refuse("bcfft_forward_glu", algo, n_in, block_size, x_dtype, x_dtype);
   if (algo == BCFFT_ALGO_DFT && !dm && !dm64)
     return refuse("bcfft_forward_glu", algo, n_in, block_size, x_dtype, x_dtype);
   if (n_tokens == 0) return BCFFT_OK;
@@ -984,7 +987,8 @@ int bcfft_forward_glu_algo(const void* x, int x_dtype, int64_t n_tokens, int in_
   else if (block_size == 64)
     bcfft::launch_forward_dm64(x, n_tokens, n_gate, spectra_gu, nullptr, BCFFT_NONE, h, true, (hipStream_t)stream);
   else
-    bcfft::launch_forward_dm_glu(block_size, n_in, x_dtype, algo == BCFFT_ALGO_DFTX, x, n_tokens, n_gate, spectra_gu,
+    bcfft::launch_forward_dm_glu(block_size, n_in, x_dtype,
+                                 algo == BCFFT_ALGO_DFTP ? 2 : algo == BCFFT_ALGO_DFTX ? 1 : 0, x, n_tokens, n_gate, spectra_gu,
                                  h, (hipStream_t)stream);
   return record_launch();
 }

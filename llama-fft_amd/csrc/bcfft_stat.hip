@@ -1036,6 +1036,53 @@ __global__ void bc_stat_image_kernel(int n_out, int n_in, float2* __restrict__ s
   }
 }
 
+// The precise engine's residual image (SpecLayout::lo8): for every element of the STAT image's B
+// fragments of the b = 128, K = 4096 geometry, e4m3(v s_o - fp16(v s_o)), v = conj(C) (fp32 packed
+// spectra). 16 B per (group, wave, bin, K-step, lane): N-tile 0's 8 elements, then N-tile 1's, in the
+// fragment order of the fp16 image (input block i0 + e, (re, im)).
+__global__ void bc_lo8_image_kernel(int n_out, const float2* __restrict__ spec, uint4* __restrict__ lo8,
+                                    const uint32_t* __restrict__ osc) {
+  constexpr int B = 128, H = 64, BW = 8, NW = 8, N_IN = 32;
+  const int groups = (n_out + STAT_OUT_BLOCKS - 1) / STAT_OUT_BLOCKS;
+  const int64_t total = (int64_t)groups * NW * BW * 2 * 64;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(idx & 63);
+    const int ks = (int)((idx >> 6) & 1);
+    const int fb = (int)((idx >> 7) % BW);
+    const int w = (int)((idx >> 7) / BW % NW);
+    const int gq = (int)((idx >> 7) / BW / NW);
+    const int f = w * BW + fb;
+    uint32_t d[4];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int o = gq * STAT_OUT_BLOCKS + nt * 16 + (lane & 15);
+      const float sc = o < n_out ? __uint_as_float((254u << 23) - osc[o]) : 1.f;
+      const int i0 = ks * 16 + 4 * (lane >> 4);
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        float r[4];
+#pragma unroll
+        for (int e2 = 0; e2 < 2; ++e2) {
+          const int i = i0 + 2 * half + e2;
+          float2 c = make_float2(0.f, 0.f);
+          if (o < n_out && i < N_IN) {
+            c = spec[((int64_t)o * N_IN + i) * H + f];
+            if (f != 0) c.y = -c.y;
+          }
+          const float vr = c.x * sc, vi = c.y * sc;
+          r[2 * e2] = vr - (float)(_Float16)vr;
+          r[2 * e2 + 1] = vi - (float)(_Float16)vi;
+        }
+        int pk = __builtin_amdgcn_cvt_pk_fp8_f32(r[0], r[1], 0, false);
+        pk = __builtin_amdgcn_cvt_pk_fp8_f32(r[2], r[3], pk, true);
+        d[2 * nt + half] = (uint32_t)pk;
+      }
+    }
+    lo8[idx] = make_uint4(d[0], d[1], d[2], d[3]);
+  }
+}
+
 }  // namespace bcfft
 
 namespace {
@@ -1114,6 +1161,16 @@ bool launch_forward_stat(int b, int n_in, int xdt, bool yf32, const void* x, int
   if (b == 128) return launch_stat_dt<128, 2>(xdt, yf32, x, n, n_out, spec, bias, bias_dt, y, s);
   if (n_in == 64) return launch_stat_dt<64, 4>(xdt, yf32, x, n, n_out, spec, bias, bias_dt, y, s);
   return launch_stat_dt<64, 2>(xdt, yf32, x, n, n_out, spec, bias, bias_dt, y, s);
+}
+
+void launch_lo8_image(int n_out, void* spec, hipStream_t s) {
+  const SpecLayout sl = spec_layout(n_out, 32, 128);
+  if (sl.lo8_u32 == 0) return;
+  const int64_t total = sl.lo8_u32 / 4;
+  const unsigned blocks = (unsigned)((total + 255) / 256 < 65535 ? (total + 255) / 256 : 65535);
+  hipLaunchKernelGGL(bc_lo8_image_kernel, dim3(blocks), dim3(256), 0, s, n_out, (const float2*)spec,
+                     reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(spec) + sl.lo8_off_u32),
+                     reinterpret_cast<const uint32_t*>(spec) + sl.osc_off_u32);
 }
 
 void launch_stat_image(int b, int n_out, int n_in, void* spec, hipStream_t s) {

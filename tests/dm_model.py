@@ -15,6 +15,11 @@ are checked on the CPU against the oracle before the GPU runs them:
            hi + lo (exact) or rounded once to fp16.
   stage 3  E = Fe Y16_even, O = Fo Y16_odd (fp32 accumulation); y_t = (E + O) sc,
            y_{t+64} = (E - O) sc with sc = 2^(30 - nmin) / s_C.
+
+precise=True mirrors the precise engine (BCFFT_ALGO_DFTP, the kernel's EP = 7 variant): the table
+is F 2^8 in fp16 (kDmFp) and a, d are scaled 2^15 lower; each fp16 single term gets its rounding
+residual back in e4m3 (kDmFl8 for the table, the lo8 image e4m3(conj(C) s_o - fp16(.)) for the
+weights), multiplied by bf8 (the fp16 value's high byte) of the other operand's fp16 terms.
 """
 import os
 import re
@@ -44,6 +49,54 @@ def _rtz16(v):
     over = np.abs(r) > np.abs(v)
     nxt = np.nextafter(r.astype(np.float16), np.float16(0)).astype(np.float64)
     return np.where(over, nxt, r)
+
+
+def dm_table_precise():
+    """(F 2^8 as the kernel's fp16 kDmFp, its e4m3 residual kDmFl8 decoded), both 64 x 128."""
+    text = open(_TABLE).read()
+
+    def words(name, n):
+        body = text[text.index(name):]
+        body = body[:body.index("};")]
+        w = np.array([int(v, 16) for v in re.findall(r"0x([0-9a-f]{8})u", body)], dtype=np.uint32)
+        assert w.size == n, (name, w.size)
+        return w
+    w = words("kDmFp[4096]", 4096).reshape(64, 64)
+    bits = np.empty((64, 128), dtype=np.uint16)
+    bits[:, 0::2] = (w & 0xFFFF).astype(np.uint16)
+    bits[:, 1::2] = (w >> 16).astype(np.uint16)
+    fp = bits.view(np.float16).astype(np.float64)
+    w8 = words("kDmFl8[2048]", 2048).reshape(32, 64)         # pair-row p, column pair
+    pairs = np.empty((32, 128), dtype=np.uint32)
+    pairs[:, 0::2] = w8 & 0xFFFF
+    pairs[:, 1::2] = w8 >> 16
+    codes = np.empty((64, 128), dtype=np.uint32)
+    codes[0::2] = pairs & 0xFF
+    codes[1::2] = pairs >> 8
+    return fp, e4m3_decode(codes)
+
+
+def e4m3_decode(codes):
+    """OCP e4m3fn codes -> float64 (no NaN codes occur here)."""
+    c = np.asarray(codes, dtype=np.int64)
+    e, m = (c >> 3) & 15, c & 7
+    v = np.where(e == 0, m / 8.0 * 2.0 ** -6, (1 + m / 8.0) * 2.0 ** (e - 7.0))
+    return np.where(c & 0x80, -v, v)
+
+
+def e4m3(v):
+    """fp32 -> OCP e4m3fn value, round to nearest even (v_cvt_pk_fp8_f32; |v| < 448 here)."""
+    v = np.asarray(v, np.float32).astype(np.float64)
+    a = np.abs(v)
+    e = np.maximum(np.floor(np.log2(np.maximum(a, 2.0 ** -40))), -6)
+    q = 2.0 ** (e - 3)
+    return np.sign(v) * np.round(a / q) * q
+
+
+def bf8(v):
+    """bf8 (e5m2) of fp16 values: the high byte, i.e. the mantissa truncated to 2 bits."""
+    h = np.asarray(v, np.float64).astype(np.float16).view(np.uint16) & np.uint16(0xFF00)
+    return h.view(np.float16).astype(np.float64)
 
 
 def _split16(v):
@@ -80,7 +133,25 @@ def _rne16(v):
     return np.asarray(v, np.float32).astype(np.float16).astype(np.float64)
 
 
-def dm_forward(x, c, exact=True, single_x=False, head=None):
+def lo8_image(c):
+    """The precise engine's weight residuals e4m3(v s_o - fp16(v s_o)) (bc_lo8_image_kernel), in
+    stat_image's layout: (re, im), the same packed bins."""
+    b = c.shape[-1]
+    h = b // 2
+    xf = np.fft.rfft(c.astype(np.float64), axis=-1) / (2.0 * b)
+    p = xf[..., :h].astype(np.complex64).astype(np.complex128)
+    p[..., 0] = np.float32(xf[..., 0].real) + 1j * np.float32(xf[..., h].real)
+    mx = np.maximum(np.abs(p.real), np.abs(p.imag)).reshape(p.shape[0], -1).max(axis=1)
+    n2 = np.array([int(np.clip(15 - np.frexp(np.float32(m))[1], -126, 126)) if m > 0 else 0 for m in mx])
+    sc = (2.0 ** n2)[:, None, None]
+    out = []
+    for part in (p.real, p.imag):
+        v = (part * sc).astype(np.float32)
+        out.append(e4m3(v.astype(np.float64) - v.astype(np.float16).astype(np.float64)))
+    return out[0], out[1]
+
+
+def dm_forward(x, c, exact=True, single_x=False, head=None, precise=False, terms=(1, 1, 1)):
     """x (N, K) float32, c (nO, nI, 128): the kernel's fp32 output (no bias). exact: the
     BCFFT_ALGO_DFTX variant (a, d and Y as hi + lo); else "dft" (one RNE term each). single_x:
     the bf16-I/O kernel of bcfft_dm8.hip, whose X is one RNE fp16 term too.
@@ -93,6 +164,8 @@ def dm_forward(x, c, exact=True, single_x=False, head=None):
     final R."""
     n, k = x.shape
     no, ni, b = c.shape
+    if precise:
+        exact = True
     if head is not None:
         single_x = True
         exact = False
@@ -104,7 +177,13 @@ def dm_forward(x, c, exact=True, single_x=False, head=None):
             k += pad * b
     assert b == 128 and ni * b == k and ni % 16 == 0
     h = 64
-    F = dm_table()
+    if precise:
+        F, FL = dm_table_precise()                                # F 2^8: the data scale 2^-15 lower
+        FLe, FLo = FL[:, :64], FL[:, 64:]
+        lre, lim = lo8_image(c)
+        t1, t2, t3 = (bool(t) for t in terms)
+    else:
+        F = dm_table()
     Fe, Fo = F[:, :64], F[:, 64:]
     cre, cim, inv_sc = stat_image(c)
     y = np.zeros((n, no * b))
@@ -112,19 +191,25 @@ def dm_forward(x, c, exact=True, single_x=False, head=None):
     for tok in range(n):
         xr = x[tok].astype(np.float32).reshape(ni, b).astype(np.float64)
         X = np.zeros((ni, h), dtype=np.complex128)
+        if precise:
+            XB = np.zeros((ni, h), dtype=np.complex128)               # bf8 of X's fp16 terms, summed
         nsc = []
         for hh in range(halves):
             blk = xr[16 * hh:16 * hh + 16]
             sx = _scale_exp(2.0 * np.abs(blk).max()) - (head or 0)
-            s = 2.0 ** sx
+            s = 2.0 ** (max(sx - 15, -126) if precise else sx)
             lo, hi = blk[:, :64], blk[:, 64:]
             a = ((lo + hi).astype(np.float32) * np.float32(s)).astype(np.float64)
             d = ((lo - hi).astype(np.float32) * np.float32(s)).astype(np.float64)
             if exact:
                 ah, al = _split16(a)
                 dh, dl = _split16(d)
-                ev = (ah @ Fe + al @ Fe).astype(np.float32)      # (16, 64): even packed bins
-                od = (dh @ Fo + dl @ Fo).astype(np.float32)
+                ev = ah @ Fe + al @ Fe                                   # (16, 64): even packed bins
+                od = dh @ Fo + dl @ Fo
+                if precise and t1:
+                    ev = ev + bf8(ah) @ FLe
+                    od = od + bf8(dh) @ FLo
+                ev, od = ev.astype(np.float32), od.astype(np.float32)
             else:
                 ev = (_rne16(a) @ Fe).astype(np.float32)
                 od = (_rne16(d) @ Fo).astype(np.float32)
@@ -137,6 +222,8 @@ def dm_forward(x, c, exact=True, single_x=False, head=None):
             else:
                 shi, slo = _split16(pk)
             X[16 * hh:16 * hh + 16] = (shi[..., 0] + slo[..., 0]) + 1j * (shi[..., 1] + slo[..., 1])
+            if precise:                        # bf8 commutes with the exact 2^-d alignment below
+                XB[16 * hh:16 * hh + 16] = (bf8(shi[..., 0]) + bf8(slo[..., 0])) + 1j * (bf8(shi[..., 1]) + bf8(slo[..., 1]))
             nsc.append(sx - 7)
         nmin = min(nsc)
         if head is not None:                                      # the running reference
@@ -145,11 +232,18 @@ def dm_forward(x, c, exact=True, single_x=False, head=None):
                 nmin = min(nmin, e + head)
         for hh in range(halves):                                  # exact power-of-two alignment
             X[16 * hh:16 * hh + 16] *= 2.0 ** (nmin - nsc[hh])
+            if precise:
+                XB[16 * hh:16 * hh + 16] *= 2.0 ** (nmin - nsc[hh])
         # stage 2: complex MAC per bin, bin 0 as two real products with the extra 1/2
         yr = np.einsum("oif,if->of", cre[..., 1:], X.real[:, 1:]) - np.einsum("oif,if->of", cim[..., 1:], X.imag[:, 1:])
         yi = np.einsum("oif,if->of", cre[..., 1:], X.imag[:, 1:]) + np.einsum("oif,if->of", cim[..., 1:], X.real[:, 1:])
         y0 = 0.5 * np.einsum("oi,i->o", cre[..., 0], X.real[:, 0])
         y64 = 0.5 * np.einsum("oi,i->o", cim[..., 0], X.imag[:, 0])
+        if precise and t2:
+            yr = yr + np.einsum("oif,if->of", lre[..., 1:], XB.real[:, 1:]) - np.einsum("oif,if->of", lim[..., 1:], XB.imag[:, 1:])
+            yi = yi + np.einsum("oif,if->of", lre[..., 1:], XB.imag[:, 1:]) + np.einsum("oif,if->of", lim[..., 1:], XB.real[:, 1:])
+            y0 = y0 + 0.5 * np.einsum("oi,i->o", lre[..., 0], XB.real[:, 0])
+            y64 = y64 + 0.5 * np.einsum("oi,i->o", lim[..., 0], XB.imag[:, 0])
         Y = np.zeros((no, 64, 2))
         Y[:, 1:, 0], Y[:, 1:, 1] = yr, yi
         Y[:, 0, 0], Y[:, 0, 1] = y0, y64
@@ -162,9 +256,16 @@ def dm_forward(x, c, exact=True, single_x=False, head=None):
         # stage 3: columns in table order
         ye = np.stack([Y16[:, 0::2, 0], Y16[:, 0::2, 1]], -1).reshape(no, 64)
         yo = np.stack([Y16[:, 1::2, 0], Y16[:, 1::2, 1]], -1).reshape(no, 64)
-        E = (ye @ Fe.T).astype(np.float32).astype(np.float64)   # (no, 64 t)
-        O = (yo @ Fo.T).astype(np.float32).astype(np.float64)
-        sc = 2.0 ** (30 - nmin) * inv_sc
+        E = ye @ Fe.T
+        O = yo @ Fo.T
+        if precise and t3:
+            yhb = bf8(yh)
+            E = E + np.stack([yhb[:, 0::2, 0], yhb[:, 0::2, 1]], -1).reshape(no, 64) @ FLe.T
+            O = O + np.stack([yhb[:, 1::2, 0], yhb[:, 1::2, 1]], -1).reshape(no, 64) @ FLo.T
+        E = E.astype(np.float32).astype(np.float64)   # (no, 64 t)
+        O = O.astype(np.float32).astype(np.float64)
+        sc = 2.0 ** ((15 if precise else 30) - nmin) * inv_sc
         yt = np.concatenate([(E + O) * sc, (E - O) * sc], -1)
         y[tok] = yt.reshape(-1)
     return y.astype(np.float32)
+

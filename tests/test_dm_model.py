@@ -62,3 +62,43 @@ def test_dmk_mirror_vs_oracle():
     mdl = dm_forward(x, c, head=4)
     for t in range(x.shape[0]):
         assert rel_err(mdl[t], ref[t]) < 6e-4, (t, rel_err(mdl[t], ref[t]))   # measured 4.3-5.0e-4
+
+
+def test_precise_tables_are_the_residual_split():
+    """kDmFp (F 2^8 in fp16) is the dftx table times 2^15 bit for bit, and kDmFl8 is the e4m3 rounding
+    of its residual: together within e4m3's 2^-4 relative step of the residual (and of 2^-10 absolute
+    for the subnormal codes) of the exact DFT."""
+    from dm_model import dm_table_precise
+    fp, fl = dm_table_precise()
+    assert np.array_equal(fp, dm_table() * 2.0 ** 15)
+    t = np.arange(64)[:, None]
+    j = np.arange(32)[None, :]
+    F = np.zeros((64, 128))
+    F[:, 0], F[:, 1] = 1.0, (-1.0) ** np.arange(64)
+    F[:, 2:64:2] = np.cos(2 * np.pi * (2 * j[:, 1:]) * t / 128)
+    F[:, 3:64:2] = -np.sin(2 * np.pi * (2 * j[:, 1:]) * t / 128)
+    F[:, 64::2] = np.cos(2 * np.pi * (2 * j + 1) * t / 128)
+    F[:, 65::2] = -np.sin(2 * np.pi * (2 * j + 1) * t / 128)
+    res = F * 2.0 ** 8 - fp
+    assert np.abs(res).max() <= 2.0 ** -4
+    assert np.all(np.abs(fl - res) <= 2.0 ** -4 * np.abs(res) + 2.0 ** -10)
+
+
+@pytest.mark.parametrize("scale", [1.0, 1e-5, 3e4])
+def test_precise_model_vs_oracle(scale):
+    """The precise engine's arithmetic (BCFFT_ALGO_DFTP): an order of magnitude under dftx's, per
+    token as well; each residual term removes its share (dftx ~2.8e-4 -> ~2.8e-5)."""
+    rng = np.random.default_rng(9)
+    x = (rng.standard_normal((6, 4096)) * scale).astype(np.float32)
+    x[1] *= 1e3
+    x[2, 100] = 500 * scale
+    c = (rng.standard_normal((32, 32, 128)) * 0.01).astype(np.float32)
+    ref = orc.bc_forward(x, c)
+    got = dm_forward(x, c, precise=True)
+    rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
+    assert rel < 5e-5, rel
+    for t in range(x.shape[0]):
+        r = np.linalg.norm(got[t] - ref[t]) / np.linalg.norm(ref[t])
+        assert r < 8e-5, (t, r)
+    partial = dm_forward(x, c, precise=True, terms=(1, 0, 1))   # no weight residual: dftx-like
+    assert np.linalg.norm(partial - ref) / np.linalg.norm(ref) > 3 * rel

@@ -17,7 +17,7 @@ from oracle import bc_oracle as O
 pytestmark = pytest.mark.gpu
 
 N_STAR, K_STAR, B_STAR = 8192, 4096, 128
-TOL = {"auto": 6e-4, "dftx": 6e-4, "dft": 6e-4, "stationary": 6e-4, "mfma": 5e-5, "valu": 2e-6}
+TOL = {"auto": 6e-4, "dftx": 6e-4, "dft": 6e-4, "dftp": 6e-5, "stationary": 6e-4, "mfma": 5e-5, "valu": 2e-6}
 TOKEN_TOL = 1e-3                 # north star, per token
 TDT = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16}
 _cache = {}
@@ -49,7 +49,7 @@ def _per_token(g, ref):
     return num / np.maximum(den, 1e-30)
 
 
-@pytest.mark.parametrize("algo", ["auto", "dftx", "dft", "stationary", "mfma", "valu"])
+@pytest.mark.parametrize("algo", ["auto", "dftx", "dftp", "dft", "stationary", "mfma", "valu"])
 def test_north_star_all_tokens_vs_oracle(dev, monkeypatch, algo):
     """4096 -> 4096, b = 128, N = batch*seq = 8192, fp32 I/O (+ bias): every token of the bench
     workload against the oracle, Frobenius and per token. AUTO is the engine bench.py times."""
@@ -134,7 +134,7 @@ def _magnitude_norms(x, c):
     return np.sqrt(np.einsum("nof,f->n", mag ** 2, w) / b)
 
 
-@pytest.mark.parametrize("algo,xdt", [("auto", "float32"), ("dftx", "float32"), ("dft", "float32"),
+@pytest.mark.parametrize("algo,xdt", [("auto", "float32"), ("dftx", "float32"), ("dftp", "float32"), ("dft", "float32"),
                                       ("stationary", "float32"), ("mfma", "float32"), ("auto", "bfloat16")])
 def test_structured_weights_per_block_and_token(dev, monkeypatch, algo, xdt):
     """from_linear weights (output blocks ~1e4 apart in norm) through the forward, errors reported
@@ -176,12 +176,14 @@ def test_structured_weights_per_block_and_token(dev, monkeypatch, algo, xdt):
     assert per_block.max() < tol, (int(per_block.argmax()), per_block.max())
     assert pt_cond.max() < tol, (int(pt_cond.argmax()), pt_cond.max())
     assert pt.max() < 50 * tol                        # gross-error guard on the raw figure
+    if algo == "dftp":                                # the precise engine: raw per token within the north star
+        assert pt.max() < TOKEN_TOL, (int(pt.argmax()), pt.max())
 
 
 DFT_GOLDEN = [nm for nm in names("fwd_") if nm.startswith(("fwd_4096sq_b128", "fwd_up_4096x11008_b128"))]
 
 
-@pytest.mark.parametrize("algo", ["dft", "dftx"])
+@pytest.mark.parametrize("algo", ["dft", "dftx", "dftp"])
 @pytest.mark.parametrize("name", DFT_GOLDEN)
 def test_golden_under_dft_engines(dev, monkeypatch, name, algo):
     """The reference's golden vectors of the DFT geometries (b = 128, K = 4096) through the module

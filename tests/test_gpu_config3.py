@@ -70,14 +70,17 @@ def test_config3_llama7b_all_linear_b128_prefill():
 
     seen = {}
     hooks = []
+
+    def keep(key):
+        def hook(m, inp, out):                      # returns None: the module's output is kept
+            seen.setdefault(key, (m, inp[0].detach().clone(), out.detach().clone()))
+        return hook
+
     for li in (0, cfg.num_hidden_layers - 1):
         layer = model.model.layers[li]
         for nm in ("q_proj", "k_proj", "v_proj", "o_proj"):
-            mod = getattr(layer.self_attn, nm)
-            hooks.append(mod.register_forward_hook(
-                lambda m, i, o, _k=(li, nm): seen.setdefault(_k, (m, i[0].detach().clone(), o.detach().clone()))))
-        hooks.append(layer.mlp.register_forward_hook(
-            lambda m, i, o, _k=(li, "mlp"): seen.setdefault(_k, (m, i[0].detach().clone(), o.detach().clone()))))
+            hooks.append(getattr(layer.self_attn, nm).register_forward_hook(keep((li, nm))))
+        hooks.append(layer.mlp.register_forward_hook(keep((li, "mlp"))))
     try:
         with torch.inference_mode():
             logits = model(input_ids=ids, attention_mask=mask).logits
