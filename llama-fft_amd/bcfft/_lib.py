@@ -76,7 +76,10 @@ _SIGNATURES = {
 }
 
 _lib = None
-_lock = threading.Lock()
+_native = None
+_lock = threading.RLock()
+# torch.ops.bcfft_native (csrc/bcfft_torch.cpp): the C++ operators over this ABI, built next to it
+TORCH_OP_PATH = os.path.join(os.path.dirname(LIB_PATH), "libbcfft_torch.so")
 
 
 def load() -> ctypes.CDLL:
@@ -100,6 +103,25 @@ def load() -> ctypes.CDLL:
             raise RuntimeError(f"libbcfft ABI {lib.bcfft_abi_version()} != expected {ABI_VERSION}")
         _lib = lib
     return _lib
+
+
+def native_op() -> bool:
+    """True once torch.ops.bcfft_native is loaded: the hot forward / forward_glu calls then go
+    through one C++ dispatcher op (argument checks, allocation, stream lookup and the launch in
+    C++) instead of ctypes. False when that library is not built, when BCFFT_NATIVE_OP=0, or when
+    BCFFT_LIB_PATH names another engine library (the operators link the in-tree libbcfft.so).
+    Either way the kernels are libbcfft.so's: there is no CPU path."""
+    global _native
+    if _native is None:
+        with _lock:
+            if _native is None:
+                ok = (os.environ.get("BCFFT_NATIVE_OP", "1") != "0" and os.path.exists(TORCH_OP_PATH)
+                      and os.path.basename(LIB_PATH) == "libbcfft.so")
+                if ok:
+                    load()                                    # the ABI version check first
+                    torch.ops.load_library(TORCH_OP_PATH)
+                _native = ok
+    return _native
 
 
 def check(status: int, what: str) -> None:

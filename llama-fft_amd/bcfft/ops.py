@@ -79,6 +79,8 @@ def forward_glu(x2d: torch.Tensor, spec_gu: torch.Tensor, block_size: int, gate_
         raise ValueError(f"bcfft.forward_glu: engine {algo!r} has no fused gate/up form "
                          "(auto, stationary, dft, dftx); run gate and up as two forwards instead")
     _lib.require_device(x2d, "bcfft.forward_glu")
+    if _lib.native_op():
+        return torch.ops.bcfft_native.forward_glu(x2d, spec_gu, block_size, gate_features, _lib.ALGOS[algo])
     n, k = x2d.shape
     if block_size > 0 and gate_features % block_size == 0 and k % block_size == 0:
         _check_spectra(spec_gu, 32 * (-(-(gate_features // block_size) // 16)), k // block_size, block_size,
@@ -189,6 +191,9 @@ def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, bl
     "valu" (exact fp32 MAC). See include/bcfft.h. split_k=False withholds the workspace, so short
     grids run unsplit (the split-K forms sum fp32 partials: not bit-identical to the unsplit launch)."""
     _lib.require_device(x2d, "bcfft.forward")
+    if _lib.native_op():                         # the same call as one C++ op (csrc/bcfft_torch.cpp)
+        return torch.ops.bcfft_native.forward(x2d, spec, bias, block_size, out_features,
+                                              _lib.ALGOS[(algo or default_algo()).lower()], split_k)
     n, k = x2d.shape
     if block_size > 0 and out_features % block_size == 0 and k % block_size == 0:
         _check_spectra(spec, out_features // block_size, k // block_size, block_size, "bcfft.forward")
