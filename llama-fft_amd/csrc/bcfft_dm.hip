@@ -188,7 +188,26 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
           reinterpret_cast<const uint4*>(kDmFl8)[tid];
     }
   }
+  // the group's inverse weight scales 1 / s_o (per output block) -> LDS
+  if (tid < 32) reinterpret_cast<float*>(lds + OS_OFF)[tid] = osc[grp_o * 32 + tid];
   f16x8 creg[BW][KS][NT];
+#ifndef BCFFT_DM_LATE_W
+#define BCFFT_DM_LATE_W 1
+#endif
+  // LATE_W: the weight fragments (256 KiB per workgroup, ~4k cycles of L2 reads) stay in flight
+  // through the first P1 (stage 1 of tile 0 on the F waves) and are waited for at a tie at the
+  // end of each P1: only the y stores of stage 3 are younger there, so the compiler's counted wait
+  // lets those fly. They are the last loads issued, so the F waves' first x DMA is waited for
+  // with vmcnt(NPIECE).
+  constexpr bool LATE_W = BCFFT_DM_LATE_W != 0;
+  auto creg_tie = [&]() {
+#pragma unroll
+    for (int fb = 0; fb < BW; ++fb)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(creg[fb][ks][nt]));
+  };
   {
     const uint4* img = reinterpret_cast<const uint4*>(stat + 4) + ((int64_t)(grp_o * NW + wave) * NPIECE) * 64 + lane;
 #pragma unroll
@@ -198,19 +217,12 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
           creg[fb][ks][nt] = __builtin_bit_cast(f16x8, img[((fb * KS + ks) * NT + nt) * 64]);
-    // pin the loads here: without a use, hipcc sinks them to their first use inside the tile loop
-    // and keeps counting them there (vmcnt(29..0) before each stage-2 MFMA), which then waits for
-    // every in-flight x DMA and y store of the iteration
-#pragma unroll
-    for (int fb = 0; fb < BW; ++fb)
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(creg[fb][ks][nt]));
+    // without LATE_W, pin the loads here: without a use, hipcc keeps counting them up to their
+    // first use inside the tile loop (vmcnt(29..0) before each stage-2 MFMA), which then waits
+    // for every in-flight x DMA and y store of the iteration
+    if constexpr (!LATE_W) creg_tie();
   }
-  // the group's inverse weight scales 1 / s_o (per output block) -> LDS (after the weight loads: its wait must not hold them back)
-  if (tid < 32) reinterpret_cast<float*>(lds + OS_OFF)[tid] = osc[grp_o * 32 + tid];
-  wait_vmcnt<0>();
+  if constexpr (!LATE_W) wait_vmcnt<0>();
   lds_barrier();
 #if defined(BCFFT_DM_PRIO) && BCFFT_DM_PRIO == 1          // experiment: I waves win arbitration
   if (!fwave) __builtin_amdgcn_s_setprio(1);
@@ -345,6 +357,9 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
               const s16x4 rl = rlv[4 * pr + mt];
               acc[4 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_bf8(__builtin_bit_cast(long, rl), pr ? b8d : b8a,
                                                                            acc[4 * pr + mt], 0, 0, 0);
+#if defined(BCFFT_DFTP_DBG) && BCFFT_DFTP_DBG == 5
+              asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+#endif
             }
           }
       }
@@ -748,14 +763,25 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
     const int sb = 1 + 6 * (it < 8 ? it : 8);       // stamp slots: iterations 0-7, then the latest
     sub_on = it == 4;
     STAMP(sb);
+#ifndef BCFFT_DM_EARLY_X
+#define BCFFT_DM_EARLY_X 1
+#endif
+    // EARLY_X: in iteration 0 the I waves have no stage 3, and region R' is free: they stream
+    // tile m + gstride's x into it at once (slot wave - 4, the slot of the F wave that would
+    // otherwise issue it after Ba), so HBM is not idle through the first stage 1; they wait for
+    // it before Bb
+    constexpr bool EARLY_X = BCFFT_DM_EARLY_X != 0 && !DMA_P1;
+    if (EARLY_X && it == 0 && !fwave && m + gstride < n_mtiles) dma_token(m + gstride, other, 0, NDMA);
     if (fwave) {
       if (have_f) {
-        wait_vmcnt<0>();                            // this wave's own x DMA (issued a phase ahead)
+        if (LATE_W && it == 0) wait_vmcnt<NPIECE>();   // tile 0's x, not the weight loads behind it
+        else wait_vmcnt<0>();                       // this wave's own x DMA (issued a phase ahead)
         stage1(region, par);
       }
     } else if (it > 0) {
       stage3(other, par ^ 1, m - gstride);
     }
+    if constexpr (LATE_W) creg_tie();               // the weights, first needed by stage 2
 #if defined(BCFFT_DM_DMAP1)
     constexpr bool dma_p1 = true;
 #else
@@ -791,7 +817,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
 #elif defined(BCFFT_DM_DMAINTER)                    // experiment: pieces between the stage-2 bins
     const bool dma2 = fwave && m + gstride < n_mtiles;
 #else                                               // one burst at the start of phase 2 (measured best)
-    if (!DMA_P1 && fwave && m + gstride < n_mtiles) dma_token(m + gstride, other, 0, NDMA);
+    if (!DMA_P1 && fwave && m + gstride < n_mtiles && !(EARLY_X && it == 0)) dma_token(m + gstride, other, 0, NDMA);
     const bool dma2 = false;
 #endif
     STAMP(sb + 3);
@@ -799,7 +825,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
 #if defined(BCFFT_DM_DMASPLIT) || defined(BCFFT_DM_DMAP1)
     if (!fwave) wait_vmcnt<0>();                    // their share of the next x has landed
 #else
-    if (DMA_P1 && !fwave) wait_vmcnt<0>();          // EP: the next tile's x (issued by this I wave) has landed
+    if ((DMA_P1 || (EARLY_X && it == 0)) && !fwave) wait_vmcnt<0>();   // the next tile's x (issued by this I wave) has landed
 #endif
     STAMP(sb + 4);
     lds_barrier();                                  // Bb: Y units complete
@@ -845,22 +871,22 @@ namespace bcfft {
 bool dm_eligible(int n_in, int b) { return b == 128 && n_in == 32; }
 
 // mode 0: dft; 1 (exact): Y as hi + lo (BCFFT_ALGO_DFTX), which fp16 outputs always take; 2: the
-// precise engine (BCFFT_ALGO_DFTP) for fp32 outputs (16-bit outputs: DFTX, whose error already sits
-// far below their rounding)
+// precise engine (BCFFT_ALGO_DFTP) for fp32 x and outputs. 16-bit outputs, and 16-bit x (whose
+// output the reference rounds to x's dtype before the bias, :266-271), run DFTX, whose error
+// already sits far below that rounding. (The 16-bit-x instantiation of the stage-1 residual also
+// computed wrong values for the second-processed half on gfx950: DESIGN.md section 6b.)
 bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, int mode, const void* x, int64_t n, int n_out,
                        const void* spec, const void* bias, int bias_dt, void* y, hipStream_t s) {
   if (!dm_eligible(n_in, b)) return false;
   const bool exact = mode >= 1;
-  if (mode == 2 && yf32) {
+  if (mode == 2 && yf32 && xdt == BCFFT_F32) {
     constexpr int P = BCFFT_DFTP_EP;
     const int bm = bias_dt == BCFFT_NONE ? 0 : bias_dt == BCFFT_F32 ? 1 : 2;
 #define BCFFT_DMP_LAUNCH(XT)                                                                              \
   (bm == 0 ? launch_dm<XT, true, true, false, P, 0>(x, n, n_out, spec, bias, bias_dt, y, s)              \
    : bm == 1 ? launch_dm<XT, true, true, false, P, 1>(x, n, n_out, spec, bias, bias_dt, y, s)            \
              : launch_dm<XT, true, true, false, P, 2>(x, n, n_out, spec, bias, bias_dt, y, s))
-    if (xdt == BCFFT_F32) BCFFT_DMP_LAUNCH(BCFFT_F32);
-    else if (xdt == BCFFT_F16) BCFFT_DMP_LAUNCH(BCFFT_F16);
-    else BCFFT_DMP_LAUNCH(BCFFT_BF16);
+    BCFFT_DMP_LAUNCH(BCFFT_F32);
 #undef BCFFT_DMP_LAUNCH
     return true;
   }

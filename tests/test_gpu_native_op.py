@@ -36,7 +36,7 @@ def test_native_forward_bit_identical(dev, monkeypatch):
             _ctypes_path(mp)
             yc = ops.forward(x, spec, bv, b, m)
         assert y.dtype == yc.dtype and torch.equal(y, yc), (k, m, b, n)
-    with pytest.raises(RuntimeError, match="spectra|block"):
+    with pytest.raises(ValueError, match="spectra"):            # as the Python path
         ops.forward(torch.zeros(3, 4096, device=dev), spec, None, 64, 4096)
 
 

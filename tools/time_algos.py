@@ -75,6 +75,8 @@ if __name__ == "__main__":
         shapes = [(11008, 4096, 64, "bf16", n) for n in (1700, 8192)]
     if "--downsmall" in sys.argv:                   # decode sizes: AUTO's floor for the streamed kernel
         shapes = [(11008, 4096, 128, "bf16", n) for n in (1, 2, 4, 8, 16, 32)]
+    if "--fp32n" in sys.argv:                       # the fp32 headline and its 1024-token shard
+        shapes = [(4096, 4096, 128, "fp32", 8192), (4096, 4096, 128, "fp32", 1024)]
     if "--pipe" in sys.argv:                        # the bf16 K = 4096 DFT kernels (dm8, dmg, dm256, dm64)
         shapes = [(4096, 4096, 128, "bf16", 8192), (4096, 11008, 128, "bf16", 8192), (4096, 4096, 256, "bf16", 8192),
                   (4096, 11008, 256, "bf16", 8192), (4096, 4096, 64, "bf16", 8192), (4096, 4096, 128, "bf16", 1024)]
