@@ -102,6 +102,18 @@ def algo_flops(n, k, m, b):
     return n * (8 * n_out * n_in * (b // 2 + 1) + (n_in + n_out) * 2.5 * b * math.log2(b))
 
 
+MFMA_PEAK_TFLOPS = 2500.0                           # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md)
+
+
+def dft_mfma_flops(n, k, m, b):
+    """Matrix-core flops of the DFT-on-MFMA formulation at b = 128 (one fp16 term per operand):
+    per token, stage 1 (n_in blocks x 64 t x 128 bin reals), stage 2 (n_in x n_out x 64 packed
+    bins x 4 real products) and stage 3 (n_out blocks x 128 t x 64 bin reals), 2 flops a MAC."""
+    n_in, n_out = k // b, m // b
+    h = b // 2
+    return 2.0 * n * (n_in * h * b + 4 * n_in * n_out * h + n_out * b * h)
+
+
 def make_layer(k, m, b, io, bias, dev, seed=1):
     from patch_llama_fft import BlockCirculantLinear
     torch.manual_seed(seed)                                   # c ~ 0.01 N(0,1), seed 1 (§8d)
@@ -300,10 +312,18 @@ def time_mlp(dev, steps, k=4096, m=11008, b=128, n=8192):
         fused = run(lambda: ops.forward_mlp(x, sgu, sd, b, m, mode="fused"))
         split = run(lambda: ops.forward_mlp(x, sgu, sd, b, m, mode="split"))
     nbytes = 2 * n * k * 2                          # x + y (the weights stream from L2)
+    # the launch's matrix-core work: gate + up (k -> 2m) and down (m -> k) in the DFT formulation
+    flops = dft_mfma_flops(n, k, 2 * m, b) + dft_mfma_flops(n, m, k, b)
+    traffic, src = load_traffic("mlp_fused", "bc_mlp_dmm_kernel")
     return {"workload": f"MLP {k}->{m}->{k} b={b} N={n} bf16-io (gate/up + SwiGLU + down)",
             "engine": "mlp_dmm (one launch)", "ms": round(fused, 4), "split_ms": round(split, 4),
             "GTok_s": round(n / (fused * 1e-3) / 1e9, 4),
-            "xy_GB_s": round(nbytes / (fused * 1e-3) / 1e9, 1)}
+            "xy_GB_s": round(nbytes / (fused * 1e-3) / 1e9, 1),
+            "mfma_roofline": {"bound": "mfma", "flops_per_launch": flops,
+                              "achieved": round(flops / (fused * 1e-3) / 1e12, 1), "peak": MFMA_PEAK_TFLOPS,
+                              "unit": "TFLOP/s", "frac": round(flops / (fused * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS, 4)},
+            "hbm": {"algorithmic_bytes": nbytes, "traffic_bytes": traffic, "traffic_src": src,
+                    "traffic_over_algorithmic": round(traffic / nbytes, 3) if traffic else None}}
 
 
 def load_traffic(tag, kernel, algo=None):
@@ -328,6 +348,7 @@ def run_variants(dev, algo, steps):
     b x shape (bf16), and config 2's fused gate/up + SwiGLU."""
     vlist = [(4096, 4096, 64, "fp32", 128, "auto"),
              (4096, 4096, 128, "bf16", 8192, "auto"),
+             (4096, 4096, 128, "fp32", 8192, "dftp"),     # the precise engine (BCFFT_PRECISE=1's AUTO)
              (4096, 4096, 128, "fp32", 8192, "dft"),
              (4096, 4096, 128, "fp32", 8192, "stationary"),
              (4096, 4096, 128, "bf16", 8192, "stationary"),

@@ -75,6 +75,8 @@ def forward_glu(x2d: torch.Tensor, spec_gu: torch.Tensor, block_size: int, gate_
     spectra(glu_weights(c_gate, c_up)). h has x2d's dtype. algo: None -> BCFFT_ALGO env (auto:
     the DFT kernel at b = 128 with K = 4096, else stationary), or "stationary" / "dft" / "dftx"."""
     algo = default_algo() if algo is None else algo
+    if algo == "auto" and x2d.dtype == torch.float32 and precise_mode() and block_size == 128 and x2d.shape[-1] == 4096:
+        algo = "dftp"
     if algo not in ("auto", "stationary", "dft", "dftx", "dftp"):
         raise ValueError(f"bcfft.forward_glu: engine {algo!r} has no fused gate/up form "
                          "(auto, stationary, dft, dftx); run gate and up as two forwards instead")
@@ -173,12 +175,33 @@ def glu_eligible(in_features: int, block_size: int, dtype: torch.dtype | None = 
 
 
 def default_algo() -> str:
-    """BCFFT_ALGO env var: auto (default) | dft | dftx | stationary | mfma | valu."""
+    """BCFFT_ALGO env var: auto (default) | dft | dftx | dftp | stationary | mfma | valu."""
     import os
     a = os.environ.get("BCFFT_ALGO", "auto").lower()
     if a not in _lib.ALGOS:
         raise ValueError(f"BCFFT_ALGO={a!r}: expected one of {sorted(_lib.ALGOS)}")
     return a
+
+
+def precise_mode() -> bool:
+    """BCFFT_PRECISE=1: AUTO picks the fp32-faithful engines for fp32 activations (the reference's
+    fp32 arithmetic class, per token): dftp at b = 128 with K = 4096 (~2.8e-5, per token ~1e-5
+    times its cancellation), the split-bf16 MFMA kernel (~1e-5) at other b <= 128, fp32 VALU above.
+    The default AUTO keeps the faster dftx / stationary engines (~3e-4, per token up to ~6e-3 on
+    near-cancelling tokens); 16-bit activations are unaffected (their output rounding dominates)."""
+    import os
+    return os.environ.get("BCFFT_PRECISE", "0") not in ("", "0")
+
+
+def resolve_algo(algo: str | None, dtype: torch.dtype, block_size: int, in_features: int) -> str:
+    """The engine name a call runs before the library's own AUTO rule: algo, else BCFFT_ALGO, with
+    BCFFT_PRECISE's choice for fp32 activations (precise_mode)."""
+    a = (algo or default_algo()).lower()
+    if a != "auto" or dtype != torch.float32 or not precise_mode():
+        return a
+    if block_size == 128 and in_features == 4096:
+        return "dftp"
+    return "mfma" if block_size <= 128 else "valu"
 
 
 def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, block_size: int,
@@ -191,9 +214,9 @@ def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, bl
     "valu" (exact fp32 MAC). See include/bcfft.h. split_k=False withholds the workspace, so short
     grids run unsplit (the split-K forms sum fp32 partials: not bit-identical to the unsplit launch)."""
     _lib.require_device(x2d, "bcfft.forward")
+    algo = resolve_algo(algo, x2d.dtype, block_size, x2d.shape[-1])
     if _lib.native_op():                         # the same call as one C++ op (csrc/bcfft_torch.cpp)
-        return torch.ops.bcfft_native.forward(x2d, spec, bias, block_size, out_features,
-                                              _lib.ALGOS[(algo or default_algo()).lower()], split_k)
+        return torch.ops.bcfft_native.forward(x2d, spec, bias, block_size, out_features, _lib.ALGOS[algo], split_k)
     n, k = x2d.shape
     if block_size > 0 and out_features % block_size == 0 and k % block_size == 0:
         _check_spectra(spec, out_features // block_size, k // block_size, block_size, "bcfft.forward")
@@ -211,7 +234,7 @@ def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, bl
             bias = bias.clone()
         bias_ptr, bias_code = bias.data_ptr(), _lib.dtype_code(bias.dtype)
     lib = _lib.load()
-    code = _lib.ALGOS[(algo or default_algo()).lower()]
+    code = _lib.ALGOS[algo]
     # split-K workspace (short grids of the MFMA and streamed-weight kernels); caller-owned, from
     # torch's allocator
     ws_bytes = lib.bcfft_forward_workspace_bytes_io(n, k, out_features, block_size, code,

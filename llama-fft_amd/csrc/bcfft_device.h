@@ -142,6 +142,25 @@ __device__ __forceinline__ int stat_scale_exp(float mx) {
   return nsc < -126 ? -126 : (nsc > 126 ? 126 : nsc);
 }
 
+// Cache policy of the streamed activations (per translation unit): with BCFFT_STREAM_POLICY=1
+// the x LDS-DMA loads are nt (each token is read once, by one CU) and the y stores sc1 (aux 16:
+// write-through, the line leaves the XCD's L2), so that neither evicts the weight fragments every
+// CU re-reads from L2 per tile (MI355X_MICROARCH.md: plain and nt stores keep the line in L2,
+// sc1 drops it; nt loads are L2-served). Measured (tools/ab_stream.py, profiles/r04_ab_stream_policy.log):
+// 6-7 % faster for the multi-group kernels that stream every group's fragments per tile (dmg,
+// dm64g, the one-launch MLP), 2-5 % slower for the VGPR-resident and K-chunk kernels, which keep
+// the default policy.
+#ifndef BCFFT_STREAM_POLICY
+#define BCFFT_STREAM_POLICY 0
+#endif
+#if BCFFT_STREAM_POLICY
+#define BCFFT_XPOL " nt"
+#define BCFFT_YAUX 16
+#else
+#define BCFFT_XPOL ""
+#define BCFFT_YAUX 0
+#endif
+
 // ------------------------------------------------------------------ LDS-DMA (inline asm)
 // hipcc neither counts an asm load in its s_waitcnt bookkeeping nor drains it at a barrier, so
 // the x stream stays in flight across compute phases; every wait on it is explicit below.

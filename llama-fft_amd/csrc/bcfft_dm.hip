@@ -89,6 +89,16 @@ __device__ __forceinline__ long bf8x8(uint32_t w0, uint32_t w1, uint32_t w2, uin
 #ifndef BCFFT_DM_LB
 #define BCFFT_DM_LB 2
 #endif
+// schedule switches of bc_forward_dm_kernel (defaults = the product; 0 for A/B builds)
+#ifndef BCFFT_DM_LATE_W
+#define BCFFT_DM_LATE_W 1                           // weight fragments waited for after the first stage 1
+#endif
+#ifndef BCFFT_DM_EARLY_X
+#define BCFFT_DM_EARLY_X 1                          // iteration 0: the I waves stream the next tile's x at once
+#endif
+#ifndef BCFFT_DM_SPLIT_FD
+#define BCFFT_DM_SPLIT_FD 1                         // pipeline fill and drain split over both waves of a slot
+#endif
 // BM: bias handling, -1 = by the runtime bias_dt (dft / dftx); 0 = none, 1 = fp32 bias, 2 = 16-bit
 // bias, its 4 consecutive values per lane read by one buffer load (the precise engine: the general
 // per-element path's address registers do not fit beside its residual operands)
@@ -99,12 +109,24 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
     const uint4* __restrict__ lo8) {
   using namespace dmk;
   static_assert(EP == 0 || EX, "the precise engine extends the exact (hi + lo) variant");
-  constexpr bool DMA_P1 = false;                    // (experiment switch: I waves issue the next x at the end of P1)
+#ifndef BCFFT_DM_DMA_P1
+#define BCFFT_DM_DMA_P1 0
+#endif
+  constexpr bool DMA_P1 = BCFFT_DM_DMA_P1 != 0;     // (experiment switch: I waves issue the next x at the end of P1)
   constexpr int ES = XTraits<XT>::ES;
   constexpr bool Y32 = YF32 || XT == BCFFT_F32;
   constexpr int ESY = Y32 ? 4 : 2;
   constexpr int NPIECE = BW * KS * NT;
   constexpr int NDMA = K * ES / 1024;               // 1-KiB LDS-DMA pieces per token
+  constexpr bool LATE_W = BCFFT_DM_LATE_W != 0;
+  constexpr bool EARLY_X = BCFFT_DM_EARLY_X != 0 && !DMA_P1;
+  // FILL_SPLIT / DRAIN_SPLIT: the pipeline's first P1 has no stage 3 and its last no stage 1, so
+  // half the waves would idle through them: the first stage 1 runs one half of each token on its
+  // F wave and the other on its I wave (fp32 x: the halves are in place independently; the
+  // prologue's x DMA is split the same way), and the last stage 3 one N-tile on each
+  // (not in the precise engine: its residual operands leave no registers for the split paths)
+  constexpr bool FILL_SPLIT = BCFFT_DM_SPLIT_FD != 0 && LATE_W && ES == 4 && EP == 0;
+  constexpr bool DRAIN_SPLIT = BCFFT_DM_SPLIT_FD != 0 && !GLU && EP == 0;
 
   ANALYSIS_INIT;
   bool sub_on = false;                              // sub-phase stamps (analysis builds: iteration 4)
@@ -154,7 +176,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
 #pragma unroll
       for (int q = q0; q < q1; ++q) {
         uint32_t keep;
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen" BCFFT_XPOL " lds\n\ts_mov_b32 m0, %0"
                      : "=&s"(keep) : "v"(vb[q & 7]), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
       }
     } else {                                        // piece q: rows 4q + (lane >> 4), 256 B each
@@ -167,14 +189,18 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
 #pragma unroll
       for (int q = q0; q < q1; ++q) {
         uint32_t keep;
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen" BCFFT_XPOL " lds\n\ts_mov_b32 m0, %0"
                      : "=&s"(keep) : "v"(vb[q & 3]), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
       }
     }
   };
 
   // ---- prologue: first tile's x (I waves), the DFT table, the stationary B fragments
-  if (fwave && wg_in_grp < n_mtiles) dma_token(wg_in_grp, lds, 0, NDMA);
+  // (with the fill split below, each wave of a slot streams the half of tile 0's x it transforms)
+  if (wg_in_grp < n_mtiles) {
+    if (FILL_SPLIT) dma_token(wg_in_grp, lds, fwave ? 0 : NDMA / 2, fwave ? NDMA / 2 : NDMA);
+    else if (fwave) dma_token(wg_in_grp, lds, 0, NDMA);
+  }
   {
     const uint4* tab = reinterpret_cast<const uint4*>(EP ? kDmFp : kDmF);
 #pragma unroll
@@ -191,15 +217,11 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
   // the group's inverse weight scales 1 / s_o (per output block) -> LDS
   if (tid < 32) reinterpret_cast<float*>(lds + OS_OFF)[tid] = osc[grp_o * 32 + tid];
   f16x8 creg[BW][KS][NT];
-#ifndef BCFFT_DM_LATE_W
-#define BCFFT_DM_LATE_W 1
-#endif
   // LATE_W: the weight fragments (256 KiB per workgroup, ~4k cycles of L2 reads) stay in flight
   // through the first P1 (stage 1 of tile 0 on the F waves) and are waited for at a tie at the
   // end of each P1: only the y stores of stage 3 are younger there, so the compiler's counted wait
   // lets those fly. They are the last loads issued, so the F waves' first x DMA is waited for
   // with vmcnt(NPIECE).
-  constexpr bool LATE_W = BCFFT_DM_LATE_W != 0;
   auto creg_tie = [&]() {
 #pragma unroll
     for (int fb = 0; fb < BW; ++fb)
@@ -230,15 +252,16 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
   if (fwave) __builtin_amdgcn_s_setprio(1);
 #endif
 
-  // ---- stage 1 (F wave, token slot s = wave): x rows -> X hi/lo units, in place, per half
-  auto stage1 = [&](char* region, int par) {
+  // ---- stage 1 (token slot tslot): x rows -> X hi/lo units, in place, per half (hmask: the
+  // halves this wave does; both for the F wave of a steady-state tile)
+  auto stage1 = [&](char* region, int par, int hmask) {
 #if defined(BCFFT_DM_MEMONLY) || (defined(BCFFT_DM_ABL) && (BCFFT_DM_ABL & 1))   // analysis builds
-    if (lane < 2) wsc[par * 8 + wave * 2 + lane] = 0;
+    if (lane < 2 && ((hmask >> lane) & 1)) wsc[par * 8 + tslot * 2 + lane] = 0;
     return;
 #endif
     const int l = opaque(lane);
     const int b16 = l & 15, g = l >> 4;
-    char* slot = region + wave * SLOT;
+    char* slot = region + tslot * SLOT;
     // transposed-read lane address of the table: row 8g + q (+ 32 ks + 4 sec), chunk
     // (8 par + 2 mt + (p >> 1)) ^ fsw(row) = (8 par + 2 mt) ^ cx
     const int q4 = (l & 15) >> 2, p4 = l & 3;
@@ -248,7 +271,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
     // pair-row 4 g + q4 (t = 8 g + 2 q4, + 1), columns 4 p4 .. 4 p4 + 3 of the tile's 16
     const int flb = FL_OFF + FL_STRIDE * (4 * g + q4) + 8 * p4;
     // X write lane bases: precision p at (4 (p ^ (g & 1)) + (q ^ phi)) units
-    const int xq = (b16 >> 2) ^ (3 * (wave >> 1));
+    const int xq = (b16 >> 2) ^ (3 * (tslot >> 1));
     const int xw0 = 128 * 4 * g + 16 * (4 * (g & 1) + xq) + 4 * (b16 & 3);
     const int xw1 = 128 * 4 * g + 16 * (4 * ((g & 1) ^ 1) + xq) + 4 * (b16 & 3);
 #pragma unroll
@@ -256,6 +279,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
       // 16-bit x sits in the slot's first 8 KiB: half 1 (bytes 4-8 KiB) goes first, so that the
       // in-place X writes of half 1 (8-16 KiB) and then half 0 (0-8 KiB) clobber nothing unread
       const int h = ES == 4 ? hh : 1 - hh;
+      if (!((hmask >> h) & 1)) continue;
       // x of blocks 16h + b16: t = 32 ks + 8 g + j and t + 64 (j < 8)
       float xv8[2][2][8];
       const char* rowp = slot + (16 * h + b16) * (B * ES);
@@ -295,7 +319,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
       const float mxf = __builtin_fmaxf(m0, m1);
       // across lanes as magnitude bits: no NaN canonicalisation around the DPP moves
       const int sx = stat_scale_exp(2.f * __uint_as_float(wave_umax(__float_as_uint(mxf))));   // |a|, |d| <= 2 max|x|
-      if (l == 0) wsc[par * 8 + wave * 2 + h] = sx - 7;     // X = D 2^-(sx - 7): the table's 2^-7
+      if (l == 0) wsc[par * 8 + tslot * 2 + h] = sx - 7;    // X = D 2^-(sx - 7): the table's 2^-7
       // EP: a 2^(sx - 15) against the table 2^8 (the same D); max|x| < 2^125 keeps the scale normal
       const float S = __int_as_float((EP ? max(sx - 15, -126) + 127 : sx + 127) << 23);
       SUBSTAMP(56 + 4 * hh);
@@ -517,7 +541,10 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
   // the slot and stored as 1 KiB contiguous buffer stores. The slot's Y units are read into
   // registers first. 16-bit y: 32 rows x 256 B in the second 8 KiB; fp32 y: N-tile 0's 16 rows
   // in the second 8 KiB, N-tile 1's in the first. (The next tile's x arrives in P2.)
-  auto stage3 = [&](char* region, int par, int64_t mp) {
+  // ntm: the N-tiles this wave does (3: both, the I wave of a steady-state tile; the last pass
+  // splits them between the slot's F and I waves, which then meet at a barrier between their Y
+  // reads and staging writes: the staging of one N-tile overlays the Y units of both)
+  auto stage3 = [&](char* region, int par, int64_t mp, int ntm) {
     const int l = opaque(lane);
     const int o16 = l & 15, g = l >> 4;
     char* slot = region + tslot * SLOT;
@@ -544,7 +571,8 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
         for (int pr = 0; pr < 2; ++pr)
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt)
-            yf[yp][ks][pr][nt] = *reinterpret_cast<const uint4*>(yb + 8192 * yp + 4096 * ks + 16 * (32 * pr + 16 * nt));
+            if ((ntm >> nt) & 1)
+              yf[yp][ks][pr][nt] = *reinterpret_cast<const uint4*>(yb + 8192 * yp + 4096 * ks + 16 * (32 * pr + 16 * nt));
     // table row reads: row 16 mt + o16, chunk (8 par + 4 ks + g) ^ fsw(o16)
     const int gx = g ^ fsw(o16);
     const char* gb = lds + F_OFF + 256 * o16;
@@ -558,6 +586,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
     f16x8 gcur[KS][2], gnxt[KS][2];
     gload(0, gcur);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // Y is in registers: the slot is free
+    if (ntm != 3) lds_barrier();                    // ... for both waves of the slot
     SUBSTAMP(55);
     SUBSTAMP(56);
     const int64_t tok = mp * TT + tslot;
@@ -593,6 +622,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
         for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt) {
+            if (!((ntm >> nt) & 1)) continue;
             E[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][0], __builtin_bit_cast(f16x8, yf[yp][ks][0][nt]), E[nt], 0, 0, 0);
             O[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][1], __builtin_bit_cast(f16x8, yf[yp][ks][1][nt]), O[nt], 0, 0, 0);
           }
@@ -607,6 +637,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
                                    __builtin_amdgcn_perm(w.y, w.x, flsel));
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
+              if (!((ntm >> nt) & 1)) continue;
               const uint4 v = yf[0][ks][pr][nt];
               f32x4& acc3 = pr ? O[nt] : E[nt];
               acc3 = __builtin_amdgcn_mfma_f32_16x16x32_fp8_bf8(fl, bf8x8(v.x, v.y, v.z, v.w), acc3, 0, 0, 0);
@@ -640,6 +671,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
       } else
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
+        if (!((ntm >> nt) & 1)) continue;
         const int o = 16 * nt + o16;
         float os[4];
 #pragma unroll
@@ -703,6 +735,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
       rdb[c] = lr * RB + 16 * ((w ^ lr) ^ (Y32 ? 2 * c : 4 * c));
 #pragma unroll
     for (int half = 0; half < (Y32 && !GLU ? 2 : 1); ++half) {   // 8 store instructions at a time
+      if (Y32 && !GLU && !((ntm >> half) & 1)) continue;
       uint4 d[8];
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
@@ -740,8 +773,9 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
 #endif
 #pragma unroll
       for (int q = 0; q < NQ; ++q)                  // byte offset of row 8 RPI half + RPI q + lr
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs,
-                                               vofs + (8 * half + q) * 1024, 0, 0);
+        if (Y32 || GLU || ((ntm >> (q >> 2)) & 1))  // 16-bit: rows of N-tile q >> 2
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs,
+                                                 vofs + (8 * half + q) * 1024, 0, BCFFT_YAUX);
     }
     SUBSTAMP(58);
   };
@@ -763,23 +797,28 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
     const int sb = 1 + 6 * (it < 8 ? it : 8);       // stamp slots: iterations 0-7, then the latest
     sub_on = it == 4;
     STAMP(sb);
-#ifndef BCFFT_DM_EARLY_X
-#define BCFFT_DM_EARLY_X 1
-#endif
     // EARLY_X: in iteration 0 the I waves have no stage 3, and region R' is free: they stream
     // tile m + gstride's x into it at once (slot wave - 4, the slot of the F wave that would
     // otherwise issue it after Ba), so HBM is not idle through the first stage 1; they wait for
-    // it before Bb
-    constexpr bool EARLY_X = BCFFT_DM_EARLY_X != 0 && !DMA_P1;
-    if (EARLY_X && it == 0 && !fwave && m + gstride < n_mtiles) dma_token(m + gstride, other, 0, NDMA);
-    if (fwave) {
+    // it before Bb. FILL_SPLIT / DRAIN_SPLIT: see the kernel's top.
+    const bool early = EARLY_X && it == 0 && !fwave && m + gstride < n_mtiles;
+    if (early) dma_token(m + gstride, other, 0, NDMA);
+    if (FILL_SPLIT && it == 0) {                    // fill: both waves of a slot, one half each
+      if (have_f) {
+        if (!fwave && early) wait_vmcnt<NPIECE + NDMA>();   // own half of tile 0's x (prologue)
+        else wait_vmcnt<NPIECE>();
+        stage1(region, par, fwave ? 1 : 2);
+      }
+    } else if (fwave) {
       if (have_f) {
         if (LATE_W && it == 0) wait_vmcnt<NPIECE>();   // tile 0's x, not the weight loads behind it
         else wait_vmcnt<0>();                       // this wave's own x DMA (issued a phase ahead)
-        stage1(region, par);
+        stage1(region, par, 3);
+      } else if (DRAIN_SPLIT) {                     // drain: the last tile's stage 3, N-tile 1
+        stage3(other, par ^ 1, m - gstride, 2);
       }
     } else if (it > 0) {
-      stage3(other, par ^ 1, m - gstride);
+      stage3(other, par ^ 1, m - gstride, DRAIN_SPLIT && !have_f ? 1 : 3);
     }
     if constexpr (LATE_W) creg_tie();               // the weights, first needed by stage 2
 #if defined(BCFFT_DM_DMAP1)

@@ -103,7 +103,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256_kernel(
 #pragma unroll
     for (int q = 0; q < NDMA; ++q) {
       uint32_t keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen" BCFFT_XPOL " lds\n\ts_mov_b32 m0, %0"
                    : "=&s"(keep) : "v"(vb[q & 7]), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
     }
   };
@@ -447,7 +447,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256_kernel(
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs, (2 * q + lr) * RB + 16 * w, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs, (2 * q + lr) * RB + 16 * w, 0, BCFFT_YAUX);
   };
 
   // Pipeline (bcfft_dm8.hip's), two workgroup barriers per M-tile; iteration it: region R =
@@ -555,7 +555,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256k_kernel(
 #pragma unroll
     for (int q = 0; q < NDMA_C; ++q) {
       uint32_t keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen" BCFFT_XPOL " lds\n\ts_mov_b32 m0, %0"
                    : "=&s"(keep) : "v"(vb[q & 7]), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
     }
   };
@@ -942,7 +942,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256k_kernel(
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dd[q]), yrs, (2 * q + lr) * RB + 16 * w, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dd[q]), yrs, (2 * q + lr) * RB + 16 * w, 0, BCFFT_YAUX);
   };
 
   // Pipeline: one step per (M-tile m of 8 tokens, chunk c), two barriers per step (rsel: the
@@ -1054,7 +1054,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256g_kernel(
 #pragma unroll
     for (int q = 0; q < NDMA; ++q) {
       uint32_t keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen" BCFFT_XPOL " lds\n\ts_mov_b32 m0, %0"
                    : "=&s"(keep) : "v"(vb[q & 7]), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
     }
   };
@@ -1429,7 +1429,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256g_kernel(
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs, (2 * q + lr) * RB + 16 * w, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs, (2 * q + lr) * RB + 16 * w, 0, BCFFT_YAUX);
   };
 
   // Pipeline per 8-token tile m (bcfft_dmg.hip's; region R = it & 1 holds its x, R' is free):

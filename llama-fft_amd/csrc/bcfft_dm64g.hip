@@ -23,6 +23,9 @@
 //
 // LDS (144,640 B): two regions x 8 token slots of 8,256 B, the 4 KiB DFT table, the scale
 // exponents, the inverse weight scales of up to 64 groups.
+#ifndef BCFFT_STREAM_POLICY
+#define BCFFT_STREAM_POLICY 1                       // nt x / sc1 y: the weight fragments stay in L2 (bcfft_device.h)
+#endif
 #include "bcfft_device.h"
 #include "bcfft_dm_table.h"
 #include "bcfft_dm_common.h"
@@ -93,7 +96,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64g_kernel(
 #pragma unroll
     for (int q = 0; q < NDMA; ++q) {
       uint32_t keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen" BCFFT_XPOL " lds\n\ts_mov_b32 m0, %0"
                    : "=&s"(keep) : "v"(vb), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
     }
   };
@@ -393,7 +396,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64g_kernel(
       const int rr = 8 * q + lr;
       uint4 v = *reinterpret_cast<const uint4*>(slot + 128 * rr + 16 * (w ^ ((rr & 15) >> 1)));
       if (lr & 1) v = make_uint4(v.z, v.w, v.x, v.y);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, vofs + q * 1024, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, vofs + q * 1024, 0, BCFFT_YAUX);
     }
   };
 

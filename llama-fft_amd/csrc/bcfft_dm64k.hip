@@ -104,7 +104,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
 #pragma unroll
       for (int q = 0; q < NDMA; ++q) {
         uint32_t keep;
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen" BCFFT_XPOL " lds\n\ts_mov_b32 m0, %0"
                      : "=&s"(keep) : "v"(0), "s"(zr), "s"(d0) : "memory");
       }
       return;
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         uint32_t keep;
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen" BCFFT_XPOL " lds\n\ts_mov_b32 m0, %0"
                      : "=&s"(keep) : "v"(vb), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
       }
     }
@@ -534,7 +534,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs, vofs + q * 1024, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs, vofs + q * 1024, 0, BCFFT_YAUX);
   };
 
   // Pipeline: one step per (M-tile m of 16 tokens, chunk c), two barriers per step (rsel: the

@@ -36,6 +36,9 @@
 //
 // LDS (149,760 B): XR and WR, each 8 token slots of 8,256 B (64 B off the 256-B bank period, as
 // in bcfft_dm8.hip), the DFT table, the scale exponents, the inverse weight scales.
+#ifndef BCFFT_STREAM_POLICY
+#define BCFFT_STREAM_POLICY 1                       // nt x / sc1 y: the weight fragments stay in L2 (bcfft_device.h)
+#endif
 #include "bcfft_device.h"
 #include "bcfft_dm_table.h"
 #include "bcfft_dm_common.h"
@@ -128,7 +131,7 @@ __global__ __launch_bounds__(512, 2) void bc_mlp_dmm_kernel(
 #pragma unroll
     for (int q = 0; q < NDMA; ++q) {
       uint32_t keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen" BCFFT_XPOL " lds\n\ts_mov_b32 m0, %0"
                    : "=&s"(keep) : "v"(vb[q & 3]), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
     }
   };
@@ -675,7 +678,7 @@ __global__ __launch_bounds__(512, 2) void bc_mlp_dmm_kernel(
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dv[q]), yrs, vofs + q * 1024, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dv[q]), yrs, vofs + q * 1024, 0, BCFFT_YAUX);
   };
 
   // Per 8-token tile m (x(m) in XR):

@@ -412,7 +412,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     for (int q = 0; q < NDMA; ++q) {
       const uint32_t dst = dst0 + q * 1024;
       uint32_t keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen" BCFFT_XPOL " lds\n\ts_mov_b32 m0, %0"
                    : "=&s"(keep) : "v"(vb[q % DP]), "s"(xrs), "s"(dst), "s"(q * 1024) : "memory");
     }
   };
@@ -560,12 +560,12 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
     if (nvalid >= G::NOG) {                         // uniform: every row of the group exists
 #pragma unroll
       for (int q = 0; q < NST; ++q)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs, yoff0 + q * RPI * B * ESY, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs, yoff0 + q * RPI * B * ESY, 0, BCFFT_YAUX);
     } else {
 #pragma unroll
       for (int q = 0; q < NST; ++q) {
         const int yoff = o0 + q * RPI < nvalid ? yoff0 + q * RPI * B * ESY : 0x7fff0000;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs, yoff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d[q]), yrs, yoff, 0, BCFFT_YAUX);
       }
     }
   };
@@ -616,7 +616,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_stat_kernel(
           hq = make_uint4(hw[0], hw[1], hw[2], hw[3]);
         }
         const int yoff = nvalid >= OPG || j0 + q * RPI < nvalid ? yoff0 + q * RPI * B * ESY : 0x7fff0000;
-        if (!ABLATE(2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hq), yrs, yoff, 0, 0);
+        if (!ABLATE(2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hq), yrs, yoff, 0, BCFFT_YAUX);
       }
     }
   };

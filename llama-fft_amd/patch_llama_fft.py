@@ -377,7 +377,8 @@ class BCFusedGateUp(nn.Module):
         # the fused launch only where bcfft_forward_glu_algo serves the geometry with the engine
         # BCFFT_ALGO names (mfma / valu have no fused form): otherwise two launches, never an error
         return (g.bias is None and u.bias is None and not grad and x.is_cuda
-                and _ops.glu_eligible(g.in_features, g.block_size, x.dtype, _ops.default_algo(), g.out_features))
+                and _ops.glu_eligible(g.in_features, g.block_size, x.dtype,
+                                      _ops.resolve_algo(None, x.dtype, g.block_size, g.in_features), g.out_features))
 
     def _spectra(self) -> torch.Tensor:
         g, u = self._gate.c, self._up.c

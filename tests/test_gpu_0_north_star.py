@@ -17,7 +17,7 @@ from oracle import bc_oracle as O
 pytestmark = pytest.mark.gpu
 
 N_STAR, K_STAR, B_STAR = 8192, 4096, 128
-TOL = {"auto": 6e-4, "dftx": 6e-4, "dft": 6e-4, "dftp": 6e-5, "stationary": 6e-4, "mfma": 5e-5, "valu": 2e-6}
+TOL = {"auto": 6e-4, "precise": 6e-5, "dftx": 6e-4, "dft": 6e-4, "dftp": 6e-5, "stationary": 6e-4, "mfma": 5e-5, "valu": 2e-6}
 TOKEN_TOL = 1e-3                 # north star, per token
 TDT = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16}
 _cache = {}
@@ -49,12 +49,13 @@ def _per_token(g, ref):
     return num / np.maximum(den, 1e-30)
 
 
-@pytest.mark.parametrize("algo", ["auto", "dftx", "dftp", "dft", "stationary", "mfma", "valu"])
+@pytest.mark.parametrize("algo", ["auto", "precise", "dftx", "dftp", "dft", "stationary", "mfma", "valu"])
 def test_north_star_all_tokens_vs_oracle(dev, monkeypatch, algo):
     """4096 -> 4096, b = 128, N = batch*seq = 8192, fp32 I/O (+ bias): every token of the bench
     workload against the oracle, Frobenius and per token. AUTO is the engine bench.py times."""
     from patch_llama_fft import BlockCirculantLinear
-    monkeypatch.setenv("BCFFT_ALGO", algo)
+    monkeypatch.setenv("BCFFT_ALGO", "auto" if algo == "precise" else algo)
+    monkeypatch.setenv("BCFFT_PRECISE", "1" if algo == "precise" else "0")
     c, bv, x, ref = _star_inputs()
     mod = BlockCirculantLinear(K_STAR, K_STAR, block_size=B_STAR, bias=True)
     with torch.no_grad():
@@ -134,7 +135,8 @@ def _magnitude_norms(x, c):
     return np.sqrt(np.einsum("nof,f->n", mag ** 2, w) / b)
 
 
-@pytest.mark.parametrize("algo,xdt", [("auto", "float32"), ("dftx", "float32"), ("dftp", "float32"), ("dft", "float32"),
+@pytest.mark.parametrize("algo,xdt", [("auto", "float32"), ("precise", "float32"), ("dftx", "float32"), ("dftp", "float32"),
+                                      ("dft", "float32"),
                                       ("stationary", "float32"), ("mfma", "float32"), ("auto", "bfloat16")])
 def test_structured_weights_per_block_and_token(dev, monkeypatch, algo, xdt):
     """from_linear weights (output blocks ~1e4 apart in norm) through the forward, errors reported
@@ -146,7 +148,8 @@ def test_structured_weights_per_block_and_token(dev, monkeypatch, algo, xdt):
         nearly cancels (the rank-1 part's projection of x close to zero) it is the weight
         spectra's fp16 rounding (~2^-12) times that cancellation, ~1e-2 on the DFT engines here
         and ~1e-4 on the split-bf16 'mfma' engine."""
-    monkeypatch.setenv("BCFFT_ALGO", algo)
+    monkeypatch.setenv("BCFFT_ALGO", "auto" if algo == "precise" else algo)
+    monkeypatch.setenv("BCFFT_PRECISE", "1" if algo == "precise" else "0")   # precise: AUTO -> dftp
     m, k, b, n = 4096, 4096, 128, 512
     mod = _structured_layer(dev, m, k, b, seed=3)
     if xdt != "float32":
@@ -176,7 +179,7 @@ def test_structured_weights_per_block_and_token(dev, monkeypatch, algo, xdt):
     assert per_block.max() < tol, (int(per_block.argmax()), per_block.max())
     assert pt_cond.max() < tol, (int(pt_cond.argmax()), pt_cond.max())
     assert pt.max() < 50 * tol                        # gross-error guard on the raw figure
-    if algo == "dftp":                                # the precise engine: raw per token within the north star
+    if algo in ("dftp", "precise"):                   # the precise engine: raw per token within the north star
         assert pt.max() < TOKEN_TOL, (int(pt.argmax()), pt.max())
 
 

@@ -56,3 +56,23 @@ def test_fused_gate_up_falls_back_under_other_engines(monkeypatch):
     assert ops.glu_eligible(4096, 128, torch.bfloat16, gate_features=11008)
     monkeypatch.setenv("BCFFT_ALGO", "auto")
     assert ops.glu_eligible(4096, 256, torch.bfloat16, gate_features=11008)
+
+
+def test_precise_mode_resolution(monkeypatch):
+    """BCFFT_PRECISE=1 makes AUTO pick the fp32-faithful engines for fp32 activations: dftp at
+    b = 128 with K = 4096, the split-bf16 MFMA kernel at other b <= 128, fp32 VALU above; 16-bit
+    activations and explicit engines are unaffected, and the fused gate/up falls back to two
+    launches where no precise fused form exists."""
+    import torch
+    from bcfft import ops
+    monkeypatch.delenv("BCFFT_ALGO", raising=False)
+    monkeypatch.setenv("BCFFT_PRECISE", "1")
+    assert ops.resolve_algo(None, torch.float32, 128, 4096) == "dftp"
+    assert ops.resolve_algo(None, torch.float32, 64, 4096) == "mfma"
+    assert ops.resolve_algo(None, torch.float32, 256, 4096) == "valu"
+    assert ops.resolve_algo(None, torch.bfloat16, 128, 4096) == "auto"
+    assert ops.resolve_algo("dftx", torch.float32, 128, 4096) == "dftx"
+    assert ops.glu_eligible(4096, 128, torch.float32, ops.resolve_algo(None, torch.float32, 128, 4096))
+    assert not ops.glu_eligible(4096, 64, torch.float32, ops.resolve_algo(None, torch.float32, 64, 4096))
+    monkeypatch.setenv("BCFFT_PRECISE", "0")
+    assert ops.resolve_algo(None, torch.float32, 128, 4096) == "auto"
