@@ -70,7 +70,7 @@ def run(k, m, b, io, n):
         _lib.check(lib.bcfft_set_stamps_stat(None), "stamps")
         st = buf.view(-1, 64).cpu().numpy().astype(np.int64)
         st = st[st[:, 0] != 0]
-        tiles = min(8, -(-n // 4) // (len(st) // 8))
+        tiles = max(1, min(8, -(-(-(-n // 4)) // max(1, len(st) // 8))))   # M-tiles per workgroup
         seg = np.zeros((len(st), tiles, 6))
         for it in range(tiles):
             base = 1 + 7 * it
@@ -91,14 +91,17 @@ def run(k, m, b, io, n):
     st, seg = stamps()
     pro = np.median(st[:, 1] - st[:, 0])
     tot = np.median(st[:, 63] - st[:, 0])
+    end = np.median(st[:, 63] - st[:, 1 + 7 * seg.shape[1]]) if seg.shape[1] < 8 else float("nan")
     wv = np.nonzero(buf.view(-1, 64).cpu().numpy()[:, 0])[0] % 8
     for w in range(8):
         sel = wv == w
         if sel.any():
-            print(f"wave {w}        " + " ".join(f"{np.median(seg[sel][:, 1:-1, j]):11.0f}" for j in range(6)))
+            mid = seg[sel][:, 1:-1] if seg.shape[1] > 2 else seg[sel]
+            print(f"wave {w}        " + " ".join(f"{np.median(mid[:, :, j]):11.0f}" for j in range(6)))
     print(f"waves {len(st)}, wall {wall:.1f} us, kernel cycles median {tot:.0f} "
           f"-> {tot / wall / 1e3:.2f} GHz implied; prologue {pro:.0f} cycles; first-tile sum "
-          f"{np.median(seg[:, 0].sum(axis=1)):.0f}, last-tile sum {np.median(seg[:, -1].sum(axis=1)):.0f}")
+          f"{np.median(seg[:, 0].sum(axis=1)):.0f}, last-tile sum {np.median(seg[:, -1].sum(axis=1)):.0f}, "
+          f"after the last tile (drain) {end:.0f}")
 
 
 if __name__ == "__main__":
