@@ -54,9 +54,9 @@ enum bcfft_dtype { BCFFT_NONE = -1, BCFFT_F32 = 0, BCFFT_F16 = 1, BCFFT_BF16 = 2
  *  DFTP: the precise engine: DFTX with the rounding residual of every single fp16 term (the DFT
  *        table in both transforms and the weight spectra) added back through fp8 MFMAs into the
  *        same fp32 accumulators: ~1e-5 relative, per token ~1e-5 times its cancellation (the
- *        reference's fp32 arithmetic class). Geometry as DFTX; fp32 x and outputs (16-bit x or
- *        outputs run DFTX, whose error already sits below the 16-bit rounding the reference
- *        applies to the output, patch_llama_fft.py:266).
+ *        reference's fp32 arithmetic class). Geometry as DFTX; fp32 x and outputs with no bias
+ *        or an fp32 bias (16-bit x, outputs or biases run DFTX, whose error already sits below
+ *        the 16-bit rounding the reference applies to the output, patch_llama_fft.py:266).
  *  AUTO: at block_size 128 with in_features 4096, DFTX for fp32 outputs (linear in x, which the
  *        fp32 backward's dx relies on) and DFT for 16-bit outputs (whose own rounding dominates);
  *        DFT on its other geometries; else STAT where eligible, else MFMA for block_size <= 128,

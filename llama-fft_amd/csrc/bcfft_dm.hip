@@ -910,7 +910,8 @@ namespace bcfft {
 bool dm_eligible(int n_in, int b) { return b == 128 && n_in == 32; }
 
 // mode 0: dft; 1 (exact): Y as hi + lo (BCFFT_ALGO_DFTX), which fp16 outputs always take; 2: the
-// precise engine (BCFFT_ALGO_DFTP) for fp32 x and outputs. 16-bit outputs, and 16-bit x (whose
+// precise engine (BCFFT_ALGO_DFTP) for fp32 x and outputs (no bias or an fp32 one). 16-bit outputs,
+// 16-bit biases, and 16-bit x (whose
 // output the reference rounds to x's dtype before the bias, :266-271), run DFTX, whose error
 // already sits far below that rounding. (The 16-bit-x instantiation of the stage-1 residual also
 // computed wrong values for the second-processed half on gfx950: DESIGN.md section 6b.)
@@ -918,15 +919,12 @@ bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, int mode, const void
                        const void* spec, const void* bias, int bias_dt, void* y, hipStream_t s) {
   if (!dm_eligible(n_in, b)) return false;
   const bool exact = mode >= 1;
-  if (mode == 2 && yf32 && xdt == BCFFT_F32) {
+  // (a 16-bit bias on fp32 x runs DFTX too: the precise engine's BM = 2 instantiation computed
+  // wrong outputs on gfx950)
+  if (mode == 2 && yf32 && xdt == BCFFT_F32 && (bias_dt == BCFFT_NONE || bias_dt == BCFFT_F32)) {
     constexpr int P = BCFFT_DFTP_EP;
-    const int bm = bias_dt == BCFFT_NONE ? 0 : bias_dt == BCFFT_F32 ? 1 : 2;
-#define BCFFT_DMP_LAUNCH(XT)                                                                              \
-  (bm == 0 ? launch_dm<XT, true, true, false, P, 0>(x, n, n_out, spec, bias, bias_dt, y, s)              \
-   : bm == 1 ? launch_dm<XT, true, true, false, P, 1>(x, n, n_out, spec, bias, bias_dt, y, s)            \
-             : launch_dm<XT, true, true, false, P, 2>(x, n, n_out, spec, bias, bias_dt, y, s))
-    BCFFT_DMP_LAUNCH(BCFFT_F32);
-#undef BCFFT_DMP_LAUNCH
+    if (bias_dt == BCFFT_NONE) launch_dm<BCFFT_F32, true, true, false, P, 0>(x, n, n_out, spec, bias, bias_dt, y, s);
+    else launch_dm<BCFFT_F32, true, true, false, P, 1>(x, n, n_out, spec, bias, bias_dt, y, s);
     return true;
   }
   // fp32 outputs with a bias add it at the store phase (BM = 1 / 2: one buffer load per 4 values);

@@ -155,3 +155,28 @@ def test_dftp_glu_vs_oracle(dev, m, n):
     ex = rel_err(hx.cpu().numpy(), ref)
     print(f"glu dftp {e:.3e} (dftx {ex:.3e})")
     assert e < 1e-4 and e < ex / 3, (e, ex)
+
+
+@pytest.mark.parametrize("algo", ["dftx", "dftp", "dft"])
+@pytest.mark.parametrize("bdt", [torch.float32, torch.bfloat16, torch.float16])
+def test_fp32_output_bias_dtypes(dev, algo, bdt):
+    """fp32 x with an fp32 / bf16 / fp16 bias (y promoted to fp32): the DFT kernels add it at the
+    store phase (BM = 1: one 16-B load per 4 values; BM = 2: 8-B loads of 16-bit values), as the
+    reference's `y + bias` after `.to(x.dtype)` (patch_llama_fft.py:266-271)."""
+    from bcfft import ops
+    rng = np.random.default_rng(17)
+    c = (rng.standard_normal((32, 32, 128)) * 0.01).astype(np.float32)
+    x = rng.standard_normal((37, 4096)).astype(np.float32)
+    bv = torch.from_numpy((rng.standard_normal(4096) * 0.1).astype(np.float32)).to(bdt)
+    spec = ops.spectra(torch.from_numpy(c).to(dev))
+    y = ops.forward(torch.from_numpy(x).to(dev), spec, bv.to(dev), 128, 4096, algo=algo)
+    assert y.dtype == torch.float32
+    ref = O.bc_forward(x, c, bv.float().numpy())
+    eng = "dftx" if algo == "dftp" and bdt != torch.float32 else algo   # a 16-bit bias: dftp runs dftx
+    nb = ops.forward(torch.from_numpy(x).to(dev), spec, None, 128, 4096, algo=eng)
+    # the bias add itself is exact in fp32: y - y_nobias == bias up to one fp32 rounding
+    d = (y - nb).cpu().numpy() - bv.float().numpy()[None, :]
+    assert np.abs(d).max() <= 2.0 ** -22 * (np.abs(y.cpu().numpy()).max() + 1.0), np.abs(d).max()
+    assert rel_err(y.cpu().numpy(), ref) < (DFTP_TOL if algo == "dftp" and bdt == torch.float32 else 6e-4)
+    if algo == "dftp" and bdt != torch.float32:   # a 16-bit bias runs the dftx kernel
+        assert torch.equal(y, ops.forward(torch.from_numpy(x).to(dev), spec, bv.to(dev), 128, 4096, algo="dftx"))
