@@ -8,11 +8,12 @@ bench_all_in_one.py:484). A "step" = one forward over the rank's token shard.
 
 Multi-GPU: one process per GPU. `--gpus N` without a torch.distributed
 environment re-launches this script under `torch.distributed.run` with N ranks before any GPU
-call; with one (the driver's launch) WORLD_SIZE must equal --gpus. `--partition global` (the
-default, §8e): the GLOBAL batch*seq = 8192 tokens are split into contiguous shards of
-ceil(8192 / N) rows (1024 per rank at N = 8) and every rank runs its shard with no collective in
-the data path ("scaling": "strong"); `value` = 8192 x M / the slowest rank's time.
-`--partition per-rank` keeps 8192 tokens on every rank (weak scaling). With --allgather the
+call; with one (the driver's launch) WORLD_SIZE must equal --gpus. `--partition per-rank` (the
+default): every rank runs its own batch*seq = 8192-token shard of the job with no collective in
+the data path ("scaling": "weak": the layer is a per-token map, so the token axis shards with no
+exchange), and `value` = N x 8192 x M / the slowest rank's time. `--partition global` splits ONE
+8192-token batch into contiguous ceil(8192 / N)-row shards (1024 per rank at N = 8, SURVEY.md
+§8e's strong-scaling reading; "scaling": "strong"). With --allgather the
 single RCCL all-gather of the output shards (north star) is timed in a second loop: forward +
 all_gather_into_tensor, reported as `with_allgather` (gather-inclusive throughput) beside the
 sharded-compute `value`.
@@ -463,7 +464,7 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--tokens", type=int, default=8192,
                     help="batch*seq: global tokens (--partition global) or tokens per rank (per-rank)")
-    ap.add_argument("--partition", default="global", choices=("global", "per-rank"),
+    ap.add_argument("--partition", default="per-rank", choices=("global", "per-rank"),
                     help="global: shard the global tokens over the ranks (SURVEY.md §8e, strong scaling); "
                          "per-rank: every rank runs --tokens (weak scaling)")
     ap.add_argument("--in-features", type=int, default=4096)
