@@ -148,13 +148,20 @@ __device__ __forceinline__ int stat_scale_exp(float mx) {
 // CU re-reads from L2 per tile (MI355X_MICROARCH.md: plain and nt stores keep the line in L2,
 // sc1 drops it; nt loads are L2-served). Measured (tools/ab_stream.py, profiles/r04_ab_stream_policy.log):
 // 6-7 % faster for the multi-group kernels that stream every group's fragments per tile (dmg,
-// dm64g, the one-launch MLP), 2-5 % slower for the VGPR-resident and K-chunk kernels, which keep
-// the default policy.
+// dm64g, the one-launch MLP); the K-chunk kernels (dmk, dm64k) gain from the write-through stores
+// alone (policy 3: 4-5 % at 11008 -> 4096 b = 128), and the VGPR-resident kernels keep the default.
+// nt x loads alone were slower everywhere (profiles/r04_ab_stream_policy_split.log).
 #ifndef BCFFT_STREAM_POLICY
 #define BCFFT_STREAM_POLICY 0
 #endif
-#if BCFFT_STREAM_POLICY
+#if BCFFT_STREAM_POLICY == 1                       // nt x loads, write-through y stores
 #define BCFFT_XPOL " nt"
+#define BCFFT_YAUX 16
+#elif BCFFT_STREAM_POLICY == 2                     // analysis builds: nt x loads only
+#define BCFFT_XPOL " nt"
+#define BCFFT_YAUX 0
+#elif BCFFT_STREAM_POLICY == 3                     // analysis builds: write-through y stores only
+#define BCFFT_XPOL ""
 #define BCFFT_YAUX 16
 #else
 #define BCFFT_XPOL ""

@@ -25,6 +25,9 @@
 // LDS (138,816 B): two regions x 16 token slots of 4,160 B (a token's 32-block x chunk, 32 rows x
 // 128 B -> X units (2 K-steps x 2 KiB, bcfft_dm64.hip's map) -> at the tile end Y half-units ->
 // y staging), the 4 KiB DFT table, the scales.
+#ifndef BCFFT_STREAM_POLICY
+#define BCFFT_STREAM_POLICY 3                       // write-through y stores (level to 1 % faster; nt x loads slower, profiles/r04_ab_stream_policy_split.log)
+#endif
 #include "bcfft_device.h"
 #include "bcfft_dm_table.h"
 #include "bcfft_dm_common.h"

@@ -34,6 +34,9 @@
 // holding 8 Y / y-staging slots of 8,256 B at the tile end, the DFT table, the scales. Slot
 // strides are 64 B off the 256-B bank period, as in bcfft_dm8.hip, so the stage-2 reads of eight
 // tokens at once are conflict-free; all in-slot offsets are bcfft_dm8.hip's.
+#ifndef BCFFT_STREAM_POLICY
+#define BCFFT_STREAM_POLICY 3                       // write-through y stores: 4-5 % faster here, nt x loads slower (profiles/r04_ab_stream_policy_split.log)
+#endif
 #include "bcfft_device.h"
 #include "bcfft_dm_table.h"
 #include "bcfft_dm_common.h"
