@@ -99,6 +99,9 @@ __device__ __forceinline__ long bf8x8(uint32_t w0, uint32_t w1, uint32_t w2, uin
 #ifndef BCFFT_DM_SPLIT_FD
 #define BCFFT_DM_SPLIT_FD 1                         // pipeline fill and drain split over both waves of a slot
 #endif
+#ifndef BCFFT_DM_SYM
+#define BCFFT_DM_SYM 0                              // every P1 split over both waves of a slot (fp32 x)
+#endif
 // BM: bias handling, -1 = by the runtime bias_dt (dft / dftx); 0 = none, 1 = fp32 bias, 2 = 16-bit
 // bias, its 4 consecutive values per lane read by one buffer load (the precise engine: the general
 // per-element path's address registers do not fit beside its residual operands)
@@ -127,6 +130,11 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
   // (not in the precise engine: its residual operands leave no registers for the split paths)
   constexpr bool FILL_SPLIT = BCFFT_DM_SPLIT_FD != 0 && LATE_W && ES == 4 && EP == 0;
   constexpr bool DRAIN_SPLIT = BCFFT_DM_SPLIT_FD != 0 && !GLU && EP == 0;
+  // SYM: the split of both, in every iteration: each wave of slot j runs stage 3 of one N-tile of
+  // the previous tile, then stage 1 of one half of the current one, and streams that half of the
+  // next tile's x in P2 (so it waits for its own DMA only). Both waves of a SIMD then carry the
+  // same P1 and P2 work.
+  constexpr bool SYM = BCFFT_DM_SYM != 0 && FILL_SPLIT && DRAIN_SPLIT && Y32;
 
   ANALYSIS_INIT;
   bool sub_on = false;                              // sub-phase stamps (analysis builds: iteration 4)
@@ -809,6 +817,12 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
         else wait_vmcnt<NPIECE>();
         stage1(region, par, fwave ? 1 : 2);
       }
+    } else if (SYM) {                               // F wave: N-tile 1 and half 0, I wave: N-tile 0 and half 1
+      stage3(other, par ^ 1, m - gstride, fwave ? 2 : 1);
+      if (have_f) {
+        wait_vmcnt<8>();                            // own half of the x (older than stage 3's 8 y stores)
+        stage1(region, par, fwave ? 1 : 2);
+      }
     } else if (fwave) {
       if (have_f) {
         if (LATE_W && it == 0) wait_vmcnt<NPIECE>();   // tile 0's x, not the weight loads behind it
@@ -856,7 +870,12 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
 #elif defined(BCFFT_DM_DMAINTER)                    // experiment: pieces between the stage-2 bins
     const bool dma2 = fwave && m + gstride < n_mtiles;
 #else                                               // one burst at the start of phase 2 (measured best)
-    if (!DMA_P1 && fwave && m + gstride < n_mtiles && !(EARLY_X && it == 0)) dma_token(m + gstride, other, 0, NDMA);
+    if (SYM) {
+      if (m + gstride < n_mtiles && !(EARLY_X && it == 0))
+        dma_token(m + gstride, other, fwave ? 0 : NDMA / 2, fwave ? NDMA / 2 : NDMA);
+    } else if (!DMA_P1 && fwave && m + gstride < n_mtiles && !(EARLY_X && it == 0)) {
+      dma_token(m + gstride, other, 0, NDMA);
+    }
     const bool dma2 = false;
 #endif
     STAMP(sb + 3);
