@@ -97,8 +97,9 @@ def test_dmk_per_token_chunk_scales(dev, n):
 
 
 def test_dmk_full_size_and_linearity(dev):
-    """11008 -> 4096, N = 8192 (the sweep's down projection): oracle parity on a slice, run-to-run
-    bit equality, and linearity over all tokens within the bf16 rounding."""
+    """11008 -> 4096, N = 8192 (the sweep's down projection): every token against the oracle
+    (~1 bf16 ulp per element, 4e-3 per token), run-to-run bit equality, and linearity over all
+    tokens within the bf16 rounding."""
     from bcfft import ops
     k, m, b, n = 11008, 4096, 128, 8192
     rng = np.random.default_rng(0)
@@ -106,9 +107,16 @@ def test_dmk_full_size_and_linearity(dev):
     spec = ops.spectra(torch.from_numpy(c).to(dev).to(torch.bfloat16))
     xt = torch.randn(n, k, device=dev).to(torch.bfloat16)
     y = ops.forward(xt, spec, None, b, m, algo="dft")
-    sl = slice(5000, 5128)
-    ref = O.bc_forward(xt[sl].float().cpu().numpy(), O.round_to(c, O.BF16), x_dtype=O.BF16)
-    assert rel_err(y[sl].float().cpu().numpy(), ref) < 4e-3
+    ref = O.bc_forward(xt.float().cpu().numpy(), O.round_to(c, O.BF16), x_dtype=O.BF16)
+    g = y.float().cpu().numpy()
+    assert rel_err(g, ref) < 4e-3
+    ulp = 2.0 ** -7
+    rms = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
+    bad = np.abs(g - ref) > 2 * ulp * np.abs(ref) + 2 * ulp * rms
+    assert not bad.any(), f"{int(bad.sum())} elements beyond ~1 ulp"
+    tok = np.sqrt(((g.astype(np.float64) - ref) ** 2).sum(1) / (ref.astype(np.float64) ** 2).sum(1))
+    print(f"dmk full size: worst token {tok.max():.3e}, Frobenius {rel_err(g, ref):.3e}")
+    assert tok.max() < 4e-3, (int(tok.argmax()), tok.max())
     assert torch.equal(y, ops.forward(xt, spec, None, b, m, algo="dft"))
     x2 = torch.randn(n, k, device=dev).to(torch.bfloat16)
     lhs = ops.forward((xt.float() + x2.float()).to(torch.bfloat16), spec, None, b, m, algo="dft").float()

@@ -117,7 +117,8 @@ def test_fused_vs_oracle(dev):
 def test_fused_full_size_llama7b(dev):
     """8192 tokens, 4096 -> 11008 -> 4096 (the reference's --bench_mlp shape at batch 4 x seq 2048):
     against the split form bit for bit (the split form's down launch takes 16-token tiles here),
-    and the first 24 tokens against the oracle."""
+    and every token against the oracle (Frobenius 4e-3 as test_fused_vs_oracle; per token 8e-3:
+    bf16 h and y roundings over 8192 tokens' tails)."""
     n, n_h = 8192, 86
     cg, cu, cd = _weights(dev, n_h, seed=21)
     torch.manual_seed(21)
@@ -128,8 +129,13 @@ def test_fused_full_size_llama7b(dev):
     d = (yf.float() - ys.float())
     assert torch.equal(yf, ys), (f"max |diff| {d.abs().max().item():.3e}, rel "
                                  f"{(d.norm() / ys.float().norm()).item():.3e}")
-    ref = oracle_mlp(x[:24].float().cpu().numpy(), cg.cpu().numpy(), cu.cpu().numpy(), cd.cpu().numpy())
-    assert rel_err(yf[:24].float().cpu().numpy(), ref) < 4e-3
+    ref = oracle_mlp(x.float().cpu().numpy(), cg.cpu().numpy(), cu.cpu().numpy(), cd.cpu().numpy())
+    g = yf.float().cpu().numpy()
+    e = rel_err(g, ref)
+    tok = np.sqrt(((g.astype(np.float64) - ref) ** 2).sum(1) / (ref.astype(np.float64) ** 2).sum(1))
+    print(f"fused MLP full size vs oracle: Frobenius {e:.3e}, worst token {tok.max():.3e}")
+    assert e < 4e-3, e
+    assert tok.max() < 8e-3, (int(tok.argmax()), tok.max())
 
 
 def test_auto_and_ineligible(dev):
