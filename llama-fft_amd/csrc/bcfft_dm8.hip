@@ -105,14 +105,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
   };
 
   // ---- prologue: first tile's x, the DFT table, the stationary B fragments
-#ifdef BCFFT_DM8_FI
-  if (wg_in_grp < n_mtiles && wave < 4) {
-    dma_token(wg_in_grp, lds, wave);
-    dma_token(wg_in_grp, lds, wave + 4);
-  }
-#else
   if (wg_in_grp < n_mtiles) dma_token(wg_in_grp, lds, wave);
-#endif
   {
     const uint4* tab = reinterpret_cast<const uint4*>(kDmF);
 #pragma unroll
@@ -510,15 +503,22 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
     // F waves 0-3: stage 1 of tokens w and w + 4; I waves 4-7: stage 3 of tokens w - 4 and w of
     // the previous tile (each SIMD then mixes one F and one I wave); the F waves stream the next
     // tile's x for their two slots after Ba (the I waves' staging reads of those slots are done)
+    // The pipeline's fill (no stage 3) and drain (no stage 1) keep one token per wave, so that
+    // no wave idles through them.
     const bool fwave = wave < 4;
-    if (fwave) {
+    if (it == 0) {                                  // fill: token w (x streamed by wave w)
       if (have) {
-        wait_vmcnt<0>();                            // this wave's own x DMA
-        STAMP(sb + 1);
+        wait_vmcnt<0>();
         stage1(region, par, wave);
-        stage1(region, par, wave + 4);
       }
-    } else if (it > 0) {
+    } else if (!have) {                             // drain: token w of the last tile
+      stage3(other, par ^ 1, m - gstride, wave);
+    } else if (fwave) {
+      wait_vmcnt<0>();                              // this wave's own x DMA (both slots)
+      STAMP(sb + 1);
+      stage1(region, par, wave);
+      stage1(region, par, wave + 4);
+    } else {
       stage3(other, par ^ 1, m - gstride, wave - 4);
       stage3(other, par ^ 1, m - gstride, wave);
     }
