@@ -99,6 +99,9 @@ __device__ __forceinline__ long bf8x8(uint32_t w0, uint32_t w1, uint32_t w2, uin
 #ifndef BCFFT_DM_SPLIT_FD
 #define BCFFT_DM_SPLIT_FD 1                         // pipeline fill and drain split over both waves of a slot
 #endif
+#ifndef BCFFT_DM_XWAIT
+#define BCFFT_DM_XWAIT 1                            // steady-state stage 1 waits for each half of x on its own
+#endif
 #ifndef BCFFT_DM_SYM
 #define BCFFT_DM_SYM 0                              // every P1 split over both waves of a slot (fp32 x)
 #endif
@@ -262,7 +265,9 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
 
   // ---- stage 1 (token slot tslot): x rows -> X hi/lo units, in place, per half (hmask: the
   // halves this wave does; both for the F wave of a steady-state tile)
-  auto stage1 = [&](char* region, int par, int hmask) {
+  // xwait (fp32 x, steady state): this wave's x DMA of the tile is in flight, pieces 0-7 = half 0
+  // first; wait for half 0 alone, then for half 1 after half 0's transform
+  auto stage1 = [&](char* region, int par, int hmask, bool xwait = false) {
 #if defined(BCFFT_DM_MEMONLY) || (defined(BCFFT_DM_ABL) && (BCFFT_DM_ABL & 1))   // analysis builds
     if (lane < 2 && ((hmask >> lane) & 1)) wsc[par * 8 + tslot * 2 + lane] = 0;
     return;
@@ -288,6 +293,12 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
       // in-place X writes of half 1 (8-16 KiB) and then half 0 (0-8 KiB) clobber nothing unread
       const int h = ES == 4 ? hh : 1 - hh;
       if (!((hmask >> h) & 1)) continue;
+      if constexpr (ES == 4) {
+        if (xwait) {
+          if (hh == 0) wait_vmcnt<NDMA / 2>();
+          else wait_vmcnt<0>();
+        }
+      }
       // x of blocks 16h + b16: t = 32 ks + 8 g + j and t + 64 (j < 8)
       float xv8[2][2][8];
       const char* rowp = slot + (16 * h + b16) * (B * ES);
@@ -825,9 +836,10 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
       }
     } else if (fwave) {
       if (have_f) {
+        constexpr bool XW = BCFFT_DM_XWAIT != 0 && ES == 4 && EP == 0;
         if (LATE_W && it == 0) wait_vmcnt<NPIECE>();   // tile 0's x, not the weight loads behind it
-        else wait_vmcnt<0>();                       // this wave's own x DMA (issued a phase ahead)
-        stage1(region, par, 3);
+        else if (!XW) wait_vmcnt<0>();              // this wave's own x DMA (issued a phase ahead)
+        stage1(region, par, 3, XW && it > 0);
       } else if (DRAIN_SPLIT) {                     // drain: the last tile's stage 3, N-tile 1
         stage3(other, par ^ 1, m - gstride, 2);
       }
