@@ -138,8 +138,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
   wait_vmcnt<0>();
   lds_barrier();
 
-  // ---- stage 1 (wave w, token slot w): x rows -> X units (one fp16 term), in place, per half
-  auto stage1 = [&](char* region, int par, int sl) {
+  // ---- stage 1 (wave w, token slot w): x rows -> X units (one fp16 term), in place, per half.
+  // xwait: this wave's x DMA of the token is in flight (pieces 0-3 = half 0, behind its older y
+  // stores): wait for half 0 alone, then for half 1 after half 0's transform
+  auto stage1 = [&](char* region, int par, int sl, bool xwait = false) {
     const int l = opaque(lane);
     const int b16 = l & 15, g = l >> 4;
     char* slot = region + sl * SLOT;
@@ -204,6 +206,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
       const int sx = stat_scale_exp(2.f * __uint_as_float(mxq[h]));
       if (l == 0) wsc[par * 16 + sl * 2 + h] = sx - 7;
 #else
+      if (xwait) {
+        if (h == 0) wait_vmcnt<NDMA / 2>();
+        else wait_vmcnt<0>();
+      }
       // x of blocks 16h + b16: t = 32 ks + 8 g + j and t + 64 (j < 8); the half's x rows are
       // exactly the bytes its X units replace
       float xv8[2][2][8];
@@ -534,9 +540,14 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
     stage2(region, par);
 #else
     if (have) {
+#if defined(BCFFT_S1_ILP) || (defined(BCFFT_DM8_XWAIT) && BCFFT_DM8_XWAIT == 0)
       wait_vmcnt<0>();                              // this wave's x (and its older y stores)
       STAMP(sb + 1);
       stage1(region, par, wave);
+#else
+      STAMP(sb + 1);
+      stage1(region, par, wave, true);              // waits per half for this wave's x (and its older y stores)
+#endif
     }
     STAMP(sb + 2);
     if (it > 0) stage3(other, par ^ 1, m - gstride, wave);
