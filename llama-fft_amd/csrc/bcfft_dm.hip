@@ -836,7 +836,11 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
       }
     } else if (fwave) {
       if (have_f) {
+#if defined(BCFFT_DM_DMASPLIT) || defined(BCFFT_DM_DMAP1)
+        constexpr bool XW = false;                  // (experiments: another wave streams part of this x)
+#else
         constexpr bool XW = BCFFT_DM_XWAIT != 0 && ES == 4 && EP == 0;
+#endif
         if (LATE_W && it == 0) wait_vmcnt<NPIECE>();   // tile 0's x, not the weight loads behind it
         else if (!XW) wait_vmcnt<0>();              // this wave's own x DMA (issued a phase ahead)
         stage1(region, par, 3, XW && it > 0);
