@@ -102,6 +102,9 @@ __device__ __forceinline__ long bf8x8(uint32_t w0, uint32_t w1, uint32_t w2, uin
 #ifndef BCFFT_DM_XWAIT
 #define BCFFT_DM_XWAIT 1                            // steady-state stage 1 waits for each half of x on its own
 #endif
+#ifndef BCFFT_DM_DMAH
+#define BCFFT_DM_DMAH 0                             // the I wave streams half 0 of the next x at the end of P1
+#endif
 #ifndef BCFFT_DM_SYM
 #define BCFFT_DM_SYM 0                              // every P1 split over both waves of a slot (fp32 x)
 #endif
@@ -138,6 +141,10 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
   // next tile's x in P2 (so it waits for its own DMA only). Both waves of a SIMD then carry the
   // same P1 and P2 work.
   constexpr bool SYM = BCFFT_DM_SYM != 0 && FILL_SPLIT && DRAIN_SPLIT && Y32;
+  // DMAH (fp32 x): the next tile's x half 0 is streamed by the slot's I wave as soon as its stage 3
+  // has emptied the slot (end of P1; it waits for it before Bb), half 1 by the F wave after Ba
+  // (waited for in stage 1 before half 1)
+  constexpr bool DMAH = BCFFT_DM_DMAH != 0 && ES == 4 && EP == 0 && !DMA_P1 && !SYM;
 
   ANALYSIS_INIT;
   bool sub_on = false;                              // sub-phase stamps (analysis builds: iteration 4)
@@ -860,6 +867,11 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       dma_token(m + gstride, other, 0, NDMA);
     }
+    const bool dmah = DMAH && it > 0 && m + gstride < n_mtiles;
+    if (dmah && !fwave) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
+      dma_token(m + gstride, other, 0, NDMA / 2);
+    }
     STAMP(sb + 1);
     if (!have_f) break;
     // EP: the first lo8 bins of stage 2, issued by every wave here (one definition point: the
@@ -890,7 +902,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
       if (m + gstride < n_mtiles && !(EARLY_X && it == 0))
         dma_token(m + gstride, other, fwave ? 0 : NDMA / 2, fwave ? NDMA / 2 : NDMA);
     } else if (!DMA_P1 && fwave && m + gstride < n_mtiles && !(EARLY_X && it == 0)) {
-      dma_token(m + gstride, other, 0, NDMA);
+      dma_token(m + gstride, other, dmah ? NDMA / 2 : 0, NDMA);
     }
     const bool dma2 = false;
 #endif
@@ -899,7 +911,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
 #if defined(BCFFT_DM_DMASPLIT) || defined(BCFFT_DM_DMAP1)
     if (!fwave) wait_vmcnt<0>();                    // their share of the next x has landed
 #else
-    if ((DMA_P1 || (EARLY_X && it == 0)) && !fwave) wait_vmcnt<0>();   // the next tile's x (issued by this I wave) has landed
+    if ((DMA_P1 || (EARLY_X && it == 0) || dmah) && !fwave) wait_vmcnt<0>();   // the next tile's x (issued by this I wave) has landed
 #endif
     STAMP(sb + 4);
     lds_barrier();                                  // Bb: Y units complete
