@@ -105,6 +105,9 @@ __device__ __forceinline__ long bf8x8(uint32_t w0, uint32_t w1, uint32_t w2, uin
 #ifndef BCFFT_DM_DMAH
 #define BCFFT_DM_DMAH 0                             // the I wave streams half 0 of the next x at the end of P1
 #endif
+#ifndef BCFFT_DM_X2ND
+#define BCFFT_DM_X2ND 0                             // x half 1 streamed later: 1 before Bb, 2 at the next P1's start
+#endif
 #ifndef BCFFT_DM_SYM
 #define BCFFT_DM_SYM 0                              // every P1 split over both waves of a slot (fp32 x)
 #endif
@@ -145,6 +148,10 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
   // has emptied the slot (end of P1; it waits for it before Bb), half 1 by the F wave after Ba
   // (waited for in stage 1 before half 1)
   constexpr bool DMAH = BCFFT_DM_DMAH != 0 && ES == 4 && EP == 0 && !DMA_P1 && !SYM;
+  // X2 (fp32 x): the F wave's x burst is split: half 0 after Ba, half 1 (first needed by stage
+  // 1's second half) before Bb (1) or at the start of the next P1 (2): half the bytes in flight
+  constexpr int X2 = (ES == 4 && EP == 0 && !DMA_P1 && !SYM && !DMAH) ? BCFFT_DM_X2ND : 0;
+  bool pend2 = false;                               // X2 == 2: half 1 of this wave's next x is due
 
   ANALYSIS_INIT;
   bool sub_on = false;                              // sub-phase stamps (analysis builds: iteration 4)
@@ -848,6 +855,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
 #else
         constexpr bool XW = BCFFT_DM_XWAIT != 0 && ES == 4 && EP == 0;
 #endif
+        if (X2 == 2 && pend2) dma_token(m, region, NDMA / 2, NDMA);
         if (LATE_W && it == 0) wait_vmcnt<NPIECE>();   // tile 0's x, not the weight loads behind it
         else if (!XW) wait_vmcnt<0>();              // this wave's own x DMA (issued a phase ahead)
         stage1(region, par, 3, XW && it > 0);
@@ -902,7 +910,10 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
       if (m + gstride < n_mtiles && !(EARLY_X && it == 0))
         dma_token(m + gstride, other, fwave ? 0 : NDMA / 2, fwave ? NDMA / 2 : NDMA);
     } else if (!DMA_P1 && fwave && m + gstride < n_mtiles && !(EARLY_X && it == 0)) {
-      dma_token(m + gstride, other, dmah ? NDMA / 2 : 0, NDMA);
+      dma_token(m + gstride, other, dmah ? NDMA / 2 : 0, X2 ? NDMA / 2 : NDMA);
+      pend2 = X2 != 0;
+    } else {
+      pend2 = false;
     }
     const bool dma2 = false;
 #endif
@@ -913,6 +924,10 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
 #else
     if ((DMA_P1 || (EARLY_X && it == 0) || dmah) && !fwave) wait_vmcnt<0>();   // the next tile's x (issued by this I wave) has landed
 #endif
+    if (X2 == 1 && pend2) {
+      dma_token(m + gstride, other, NDMA / 2, NDMA);
+      pend2 = false;
+    }
     STAMP(sb + 4);
     lds_barrier();                                  // Bb: Y units complete
     STAMP(sb + 5);
