@@ -904,7 +904,8 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
 #elif defined(BCFFT_DM_DMAP1)                       // experiment: I waves issue it at the end of P1
     const bool dma2 = false;
 #elif defined(BCFFT_DM_DMAINTER)                    // experiment: pieces between the stage-2 bins
-    const bool dma2 = fwave && m + gstride < n_mtiles;
+    const bool dma2 = fwave && m + gstride < n_mtiles && !(EARLY_X && it == 0) && EP == 0;
+    if (EP != 0 && fwave && m + gstride < n_mtiles && !(EARLY_X && it == 0)) dma_token(m + gstride, other, 0, NDMA);
 #else                                               // one burst at the start of phase 2 (measured best)
     if (SYM) {
       if (m + gstride < n_mtiles && !(EARLY_X && it == 0))
