@@ -108,6 +108,9 @@ __device__ __forceinline__ long bf8x8(uint32_t w0, uint32_t w1, uint32_t w2, uin
 #ifndef BCFFT_DM_X2ND
 #define BCFFT_DM_X2ND 0                             // x half 1 streamed later: 1 before Bb, 2 at the next P1's start
 #endif
+#ifndef BCFFT_DM_FLAGX
+#define BCFFT_DM_FLAGX 0                            // I wave streams x half 0 at the end of P1, publishes it by an LDS flag
+#endif
 #ifndef BCFFT_DM_SYM
 #define BCFFT_DM_SYM 0                              // every P1 split over both waves of a slot (fp32 x)
 #endif
@@ -152,6 +155,13 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
   // 1's second half) before Bb (1) or at the start of the next P1 (2): half the bytes in flight
   constexpr int X2 = (ES == 4 && EP == 0 && !DMA_P1 && !SYM && !DMAH) ? BCFFT_DM_X2ND : 0;
   bool pend2 = false;                               // X2 == 2: half 1 of this wave's next x is due
+  // FLAGX (fp32 x): the slot's I wave streams half 0 of the next tile's x as soon as its stage 3
+  // has emptied the slot (end of P1), waits for it at the start of the next P1 and publishes it
+  // by writing the tile index into an LDS word, which the F wave polls before its stage 1 (the
+  // FULL-word hand-off of MI355X_MICROARCH.md's ring); half 1 stays the F wave's own P2 DMA, so
+  // no wave waits for x before Bb
+  constexpr bool FLAGX = BCFFT_DM_FLAGX != 0 && ES == 4 && EP == 0 && EARLY_X && FILL_SPLIT && !DMA_P1 && !SYM &&
+                         !DMAH && X2 == 0;
 
   ANALYSIS_INIT;
   bool sub_on = false;                              // sub-phase stamps (analysis builds: iteration 4)
@@ -160,13 +170,14 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
 #else
 #define SUBSTAMP(id) do { if (sub_on) STAMP(id); } while (0)
 #endif
-  __shared__ __attribute__((aligned(16))) char lds[EP ? LDS_BYTES_EP : LDS_BYTES];
+  __shared__ __attribute__((aligned(16))) char lds[(EP ? LDS_BYTES_EP : LDS_BYTES) + (BCFFT_DM_FLAGX ? 16 : 0)];
   int* wsc = reinterpret_cast<int*>(lds + SC_OFF);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool fwave = wave < 4;                      // F waves: stage 1 of token slot `wave`
   const int tslot = wave & 3;                       // I waves: stage 3 of token slot wave - 4
+  volatile int* xflag = reinterpret_cast<volatile int*>(lds + (EP ? LDS_BYTES_EP : LDS_BYTES)) + tslot;
   // GLU (fused gate/up + SwiGLU): n_out counts h blocks; group g holds gate blocks [16g, 16g+16)
   // in N-tile 0 and the matching up blocks in N-tile 1, and stores 16 h rows
   constexpr int OPG = GLU ? NOG / 2 : NOG;          // output blocks stored per group
@@ -241,6 +252,9 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
   }
   // the group's inverse weight scales 1 / s_o (per output block) -> LDS
   if (tid < 32) reinterpret_cast<float*>(lds + OS_OFF)[tid] = osc[grp_o * 32 + tid];
+#if BCFFT_DM_FLAGX
+  if (tid < 4) reinterpret_cast<int*>(lds + (EP ? LDS_BYTES_EP : LDS_BYTES))[tid] = -1;
+#endif
   f16x8 creg[BW][KS][NT];
   // LATE_W: the weight fragments (256 KiB per workgroup, ~4k cycles of L2 reads) stay in flight
   // through the first P1 (stage 1 of tile 0 on the F waves) and are waited for at a tie at the
@@ -836,6 +850,10 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
     // it before Bb. FILL_SPLIT / DRAIN_SPLIT: see the kernel's top.
     const bool early = EARLY_X && it == 0 && !fwave && m + gstride < n_mtiles;
     if (early) dma_token(m + gstride, other, 0, NDMA);
+    if (FLAGX && !fwave && it >= 2 && have_f) {     // half 0 of this tile's x (issued at the end of the last P1)
+      wait_vmcnt<0>();
+      if (lane == 0) *xflag = (int)m;
+    }
     if (FILL_SPLIT && it == 0) {                    // fill: both waves of a slot, one half each
       if (have_f) {
         if (!fwave && early) wait_vmcnt<NPIECE + NDMA>();   // own half of tile 0's x (prologue)
@@ -856,6 +874,13 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
         constexpr bool XW = BCFFT_DM_XWAIT != 0 && ES == 4 && EP == 0;
 #endif
         if (X2 == 2 && pend2) dma_token(m, region, NDMA / 2, NDMA);
+        if (FLAGX && it >= 1) {                     // half 0 of x published by this slot's I wave
+          for (int i = 0; i < (1 << 22); ++i) {
+            if (__builtin_amdgcn_readfirstlane(*xflag) == (int)m) break;
+            __builtin_amdgcn_s_sleep(2);
+          }
+          asm volatile("" ::: "memory");
+        }
         if (LATE_W && it == 0) wait_vmcnt<NPIECE>();   // tile 0's x, not the weight loads behind it
         else if (!XW) wait_vmcnt<0>();              // this wave's own x DMA (issued a phase ahead)
         stage1(region, par, 3, XW && it > 0);
@@ -876,6 +901,10 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
       dma_token(m + gstride, other, 0, NDMA);
     }
     const bool dmah = DMAH && it > 0 && m + gstride < n_mtiles;
+    if (FLAGX && !fwave && it > 0 && m + gstride < n_mtiles) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
+      dma_token(m + gstride, other, 0, NDMA / 2);
+    }
     if (dmah && !fwave) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
       dma_token(m + gstride, other, 0, NDMA / 2);
@@ -911,7 +940,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
       if (m + gstride < n_mtiles && !(EARLY_X && it == 0))
         dma_token(m + gstride, other, fwave ? 0 : NDMA / 2, fwave ? NDMA / 2 : NDMA);
     } else if (!DMA_P1 && fwave && m + gstride < n_mtiles && !(EARLY_X && it == 0)) {
-      dma_token(m + gstride, other, dmah ? NDMA / 2 : 0, X2 ? NDMA / 2 : NDMA);
+      dma_token(m + gstride, other, (dmah || (FLAGX && it > 0)) ? NDMA / 2 : 0, X2 ? NDMA / 2 : NDMA);
       pend2 = X2 != 0;
     } else {
       pend2 = false;
@@ -924,6 +953,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
     if (!fwave) wait_vmcnt<0>();                    // their share of the next x has landed
 #else
     if ((DMA_P1 || (EARLY_X && it == 0) || dmah) && !fwave) wait_vmcnt<0>();   // the next tile's x (issued by this I wave) has landed
+    if (FLAGX && early && lane == 0) *xflag = (int)(m + gstride);
 #endif
     if (X2 == 1 && pend2) {
       dma_token(m + gstride, other, NDMA / 2, NDMA);
