@@ -83,8 +83,8 @@ __device__ __forceinline__ long bf8x8(uint32_t w0, uint32_t w1, uint32_t w2, uin
 //   * stage 2 adds A(bf8) x e4m3(conj(C) s_o - fp16(conj(C) s_o)) (the lo8 image, streamed from L2
 //     by every wave for its bins, four bins ahead) to the fp16 product's accumulator;
 //   * stage 3 adds e4m3 table residual x bf8(Y hi).
-// The x DMA is issued by the I waves at the end of P1, so an F wave issues no asm VMEM operation
-// and the compiler's counted waits on its lo8 loads are exact. Numpy mirror: tests/dm_model.py
+// The F waves' x DMA (asm, invisible to the compiler's counters) is issued after Ba, once the
+// first lo8 loads of stage 2 have been waited for. Numpy mirror: tests/dm_model.py
 // (precise=True); error ~1e-5 relative (north star 1e-3), per token ~1e-5 x its cancellation.
 #ifndef BCFFT_DM_LB
 #define BCFFT_DM_LB 2
@@ -102,18 +102,6 @@ __device__ __forceinline__ long bf8x8(uint32_t w0, uint32_t w1, uint32_t w2, uin
 #ifndef BCFFT_DM_XWAIT
 #define BCFFT_DM_XWAIT 1                            // steady-state stage 1 waits for each half of x on its own
 #endif
-#ifndef BCFFT_DM_DMAH
-#define BCFFT_DM_DMAH 0                             // the I wave streams half 0 of the next x at the end of P1
-#endif
-#ifndef BCFFT_DM_X2ND
-#define BCFFT_DM_X2ND 0                             // x half 1 streamed later: 1 before Bb, 2 at the next P1's start
-#endif
-#ifndef BCFFT_DM_FLAGX
-#define BCFFT_DM_FLAGX 0                            // I wave streams x half 0 at the end of P1, publishes it by an LDS flag
-#endif
-#ifndef BCFFT_DM_SYM
-#define BCFFT_DM_SYM 0                              // every P1 split over both waves of a slot (fp32 x)
-#endif
 // BM: bias handling, -1 = by the runtime bias_dt (dft / dftx); 0 = none, 1 = fp32 bias, 2 = 16-bit
 // bias, its 4 consecutive values per lane read by one buffer load (the precise engine: the general
 // per-element path's address registers do not fit beside its residual operands)
@@ -124,17 +112,13 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
     const uint4* __restrict__ lo8) {
   using namespace dmk;
   static_assert(EP == 0 || EX, "the precise engine extends the exact (hi + lo) variant");
-#ifndef BCFFT_DM_DMA_P1
-#define BCFFT_DM_DMA_P1 0
-#endif
-  constexpr bool DMA_P1 = BCFFT_DM_DMA_P1 != 0;     // (experiment switch: I waves issue the next x at the end of P1)
   constexpr int ES = XTraits<XT>::ES;
   constexpr bool Y32 = YF32 || XT == BCFFT_F32;
   constexpr int ESY = Y32 ? 4 : 2;
   constexpr int NPIECE = BW * KS * NT;
   constexpr int NDMA = K * ES / 1024;               // 1-KiB LDS-DMA pieces per token
   constexpr bool LATE_W = BCFFT_DM_LATE_W != 0;
-  constexpr bool EARLY_X = BCFFT_DM_EARLY_X != 0 && !DMA_P1;
+  constexpr bool EARLY_X = BCFFT_DM_EARLY_X != 0;
   // FILL_SPLIT / DRAIN_SPLIT: the pipeline's first P1 has no stage 3 and its last no stage 1, so
   // half the waves would idle through them: the first stage 1 runs one half of each token on its
   // F wave and the other on its I wave (fp32 x: the halves are in place independently; the
@@ -142,26 +126,8 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
   // (not in the precise engine: its residual operands leave no registers for the split paths)
   constexpr bool FILL_SPLIT = BCFFT_DM_SPLIT_FD != 0 && LATE_W && ES == 4 && EP == 0;
   constexpr bool DRAIN_SPLIT = BCFFT_DM_SPLIT_FD != 0 && !GLU && EP == 0;
-  // SYM: the split of both, in every iteration: each wave of slot j runs stage 3 of one N-tile of
-  // the previous tile, then stage 1 of one half of the current one, and streams that half of the
-  // next tile's x in P2 (so it waits for its own DMA only). Both waves of a SIMD then carry the
-  // same P1 and P2 work.
-  constexpr bool SYM = BCFFT_DM_SYM != 0 && FILL_SPLIT && DRAIN_SPLIT && Y32;
-  // DMAH (fp32 x): the next tile's x half 0 is streamed by the slot's I wave as soon as its stage 3
-  // has emptied the slot (end of P1; it waits for it before Bb), half 1 by the F wave after Ba
-  // (waited for in stage 1 before half 1)
-  constexpr bool DMAH = BCFFT_DM_DMAH != 0 && ES == 4 && EP == 0 && !DMA_P1 && !SYM;
-  // X2 (fp32 x): the F wave's x burst is split: half 0 after Ba, half 1 (first needed by stage
-  // 1's second half) before Bb (1) or at the start of the next P1 (2): half the bytes in flight
-  constexpr int X2 = (ES == 4 && EP == 0 && !DMA_P1 && !SYM && !DMAH) ? BCFFT_DM_X2ND : 0;
-  bool pend2 = false;                               // X2 == 2: half 1 of this wave's next x is due
-  // FLAGX (fp32 x): the slot's I wave streams half 0 of the next tile's x as soon as its stage 3
-  // has emptied the slot (end of P1), waits for it at the start of the next P1 and publishes it
-  // by writing the tile index into an LDS word, which the F wave polls before its stage 1 (the
-  // FULL-word hand-off of MI355X_MICROARCH.md's ring); half 1 stays the F wave's own P2 DMA, so
-  // no wave waits for x before Bb
-  constexpr bool FLAGX = BCFFT_DM_FLAGX != 0 && ES == 4 && EP == 0 && EARLY_X && FILL_SPLIT && !DMA_P1 && !SYM &&
-                         !DMAH && X2 == 0;
+  // (round 4 measured and rejected other x-DMA placements and role splits: DESIGN.md section 8c,
+  // item 8, with their A/B logs; their switches are in the git history of this file)
 
   ANALYSIS_INIT;
   bool sub_on = false;                              // sub-phase stamps (analysis builds: iteration 4)
@@ -170,14 +136,13 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
 #else
 #define SUBSTAMP(id) do { if (sub_on) STAMP(id); } while (0)
 #endif
-  __shared__ __attribute__((aligned(16))) char lds[(EP ? LDS_BYTES_EP : LDS_BYTES) + (BCFFT_DM_FLAGX ? 16 : 0)];
+  __shared__ __attribute__((aligned(16))) char lds[EP ? LDS_BYTES_EP : LDS_BYTES];
   int* wsc = reinterpret_cast<int*>(lds + SC_OFF);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool fwave = wave < 4;                      // F waves: stage 1 of token slot `wave`
   const int tslot = wave & 3;                       // I waves: stage 3 of token slot wave - 4
-  volatile int* xflag = reinterpret_cast<volatile int*>(lds + (EP ? LDS_BYTES_EP : LDS_BYTES)) + tslot;
   // GLU (fused gate/up + SwiGLU): n_out counts h blocks; group g holds gate blocks [16g, 16g+16)
   // in N-tile 0 and the matching up blocks in N-tile 1, and stores 16 h rows
   constexpr int OPG = GLU ? NOG / 2 : NOG;          // output blocks stored per group
@@ -252,9 +217,6 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
   }
   // the group's inverse weight scales 1 / s_o (per output block) -> LDS
   if (tid < 32) reinterpret_cast<float*>(lds + OS_OFF)[tid] = osc[grp_o * 32 + tid];
-#if BCFFT_DM_FLAGX
-  if (tid < 4) reinterpret_cast<int*>(lds + (EP ? LDS_BYTES_EP : LDS_BYTES))[tid] = -1;
-#endif
   f16x8 creg[BW][KS][NT];
   // LATE_W: the weight fragments (256 KiB per workgroup, ~4k cycles of L2 reads) stay in flight
   // through the first P1 (stage 1 of tile 0 on the F waves) and are waited for at a tie at the
@@ -285,11 +247,6 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
   }
   if constexpr (!LATE_W) wait_vmcnt<0>();
   lds_barrier();
-#if defined(BCFFT_DM_PRIO) && BCFFT_DM_PRIO == 1          // experiment: I waves win arbitration
-  if (!fwave) __builtin_amdgcn_s_setprio(1);
-#elif defined(BCFFT_DM_PRIO) && BCFFT_DM_PRIO == 2        // experiment: F waves win arbitration
-  if (fwave) __builtin_amdgcn_s_setprio(1);
-#endif
 
   // ---- stage 1 (token slot tslot): x rows -> X hi/lo units, in place, per half (hmask: the
   // halves this wave does; both for the F wave of a steady-state tile)
@@ -478,11 +435,8 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
 
   // ---- stage 2 (all waves): per-bin complex MAC on bins f = 8 wave + fb; Y units over the
   // wave's own K-step-0 X units (the wave's DS operations execute in order)
-  // dma_next: this F wave streams the next tile's x into its slot of `dregion`, a piece or two
-  // per bin (spreads the x traffic over the phase instead of one burst at its start)
-  auto stage2 = [&](char* region, int par, bool dma_next, int64_t mnext, char* dregion, ClRing& clr) {
+  auto stage2 = [&](char* region, int par, ClRing& clr) {
 #if defined(BCFFT_DM_MEMONLY) || (defined(BCFFT_DM_ABL) && (BCFFT_DM_ABL & 2))
-    if (dma_next) dma_token(mnext, dregion, 0, NDMA);
     return;
 #endif
     const int ml = opaque(lane);
@@ -525,7 +479,6 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
 #pragma unroll
     for (int fb = 0; fb < BW; ++fb) {
       const int f = wave * BW + fb;
-      if (dma_next) dma_token(mnext, dregion, fb * (NDMA / BW), (fb + 1) * (NDMA / BW));
       if constexpr (EP != 0) a_load(fb);
       f32x4 acc[NT];
 #pragma unroll
@@ -850,37 +803,15 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
     // it before Bb. FILL_SPLIT / DRAIN_SPLIT: see the kernel's top.
     const bool early = EARLY_X && it == 0 && !fwave && m + gstride < n_mtiles;
     if (early) dma_token(m + gstride, other, 0, NDMA);
-    if (FLAGX && !fwave && it >= 2 && have_f) {     // half 0 of this tile's x (issued at the end of the last P1)
-      wait_vmcnt<0>();
-      if (lane == 0) *xflag = (int)m;
-    }
     if (FILL_SPLIT && it == 0) {                    // fill: both waves of a slot, one half each
       if (have_f) {
         if (!fwave && early) wait_vmcnt<NPIECE + NDMA>();   // own half of tile 0's x (prologue)
         else wait_vmcnt<NPIECE>();
         stage1(region, par, fwave ? 1 : 2);
       }
-    } else if (SYM) {                               // F wave: N-tile 1 and half 0, I wave: N-tile 0 and half 1
-      stage3(other, par ^ 1, m - gstride, fwave ? 2 : 1);
-      if (have_f) {
-        wait_vmcnt<8>();                            // own half of the x (older than stage 3's 8 y stores)
-        stage1(region, par, fwave ? 1 : 2);
-      }
     } else if (fwave) {
       if (have_f) {
-#if defined(BCFFT_DM_DMASPLIT) || defined(BCFFT_DM_DMAP1)
-        constexpr bool XW = false;                  // (experiments: another wave streams part of this x)
-#else
         constexpr bool XW = BCFFT_DM_XWAIT != 0 && ES == 4 && EP == 0;
-#endif
-        if (X2 == 2 && pend2) dma_token(m, region, NDMA / 2, NDMA);
-        if (FLAGX && it >= 1) {                     // half 0 of x published by this slot's I wave
-          for (int i = 0; i < (1 << 22); ++i) {
-            if (__builtin_amdgcn_readfirstlane(*xflag) == (int)m) break;
-            __builtin_amdgcn_s_sleep(2);
-          }
-          asm volatile("" ::: "memory");
-        }
         if (LATE_W && it == 0) wait_vmcnt<NPIECE>();   // tile 0's x, not the weight loads behind it
         else if (!XW) wait_vmcnt<0>();              // this wave's own x DMA (issued a phase ahead)
         stage1(region, par, 3, XW && it > 0);
@@ -891,24 +822,6 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
       stage3(other, par ^ 1, m - gstride, DRAIN_SPLIT && !have_f ? 1 : 3);
     }
     if constexpr (LATE_W) creg_tie();               // the weights, first needed by stage 2
-#if defined(BCFFT_DM_DMAP1)
-    constexpr bool dma_p1 = true;
-#else
-    constexpr bool dma_p1 = DMA_P1;
-#endif
-    if (dma_p1 && !fwave && m + gstride < n_mtiles) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      dma_token(m + gstride, other, 0, NDMA);
-    }
-    const bool dmah = DMAH && it > 0 && m + gstride < n_mtiles;
-    if (FLAGX && !fwave && it > 0 && m + gstride < n_mtiles) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
-      dma_token(m + gstride, other, 0, NDMA / 2);
-    }
-    if (dmah && !fwave) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
-      dma_token(m + gstride, other, 0, NDMA / 2);
-    }
     STAMP(sb + 1);
     if (!have_f) break;
     // EP: the first lo8 bins of stage 2, issued by every wave here (one definition point: the
@@ -925,40 +838,12 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
       for (int i = 0; i < RING; ++i) asm volatile("" : "+v"(clr[i][0]), "+v"(clr[i][1]));
     }
     STAMP(sb + 2);
-    // F wave j streams the next tile's x for its slot j of the other region: stage 3 has read
-    // that slot's Y and staged y (each wave's LDS reads completed before Ba)
-#if defined(BCFFT_DM_DMASPLIT)                    // experiment: F and I waves each issue half
-    if (m + gstride < n_mtiles) dma_token(m + gstride, other, fwave ? 0 : NDMA / 2, fwave ? NDMA / 2 : NDMA);
-    const bool dma2 = false;
-#elif defined(BCFFT_DM_DMAP1)                       // experiment: I waves issue it at the end of P1
-    const bool dma2 = false;
-#elif defined(BCFFT_DM_DMAINTER)                    // experiment: pieces between the stage-2 bins
-    const bool dma2 = fwave && m + gstride < n_mtiles && !(EARLY_X && it == 0) && EP == 0;
-    if (EP != 0 && fwave && m + gstride < n_mtiles && !(EARLY_X && it == 0)) dma_token(m + gstride, other, 0, NDMA);
-#else                                               // one burst at the start of phase 2 (measured best)
-    if (SYM) {
-      if (m + gstride < n_mtiles && !(EARLY_X && it == 0))
-        dma_token(m + gstride, other, fwave ? 0 : NDMA / 2, fwave ? NDMA / 2 : NDMA);
-    } else if (!DMA_P1 && fwave && m + gstride < n_mtiles && !(EARLY_X && it == 0)) {
-      dma_token(m + gstride, other, (dmah || (FLAGX && it > 0)) ? NDMA / 2 : 0, X2 ? NDMA / 2 : NDMA);
-      pend2 = X2 != 0;
-    } else {
-      pend2 = false;
-    }
-    const bool dma2 = false;
-#endif
+    // F wave j streams the next tile's x for its slot j of the other region in one burst: stage 3
+    // has read that slot's Y and staged y (each wave's LDS reads completed before Ba)
+    if (fwave && m + gstride < n_mtiles && !(EARLY_X && it == 0)) dma_token(m + gstride, other, 0, NDMA);
     STAMP(sb + 3);
-    stage2(region, par, dma2, m + gstride, other, clr);
-#if defined(BCFFT_DM_DMASPLIT) || defined(BCFFT_DM_DMAP1)
-    if (!fwave) wait_vmcnt<0>();                    // their share of the next x has landed
-#else
-    if ((DMA_P1 || (EARLY_X && it == 0) || dmah) && !fwave) wait_vmcnt<0>();   // the next tile's x (issued by this I wave) has landed
-    if (FLAGX && early && lane == 0) *xflag = (int)(m + gstride);
-#endif
-    if (X2 == 1 && pend2) {
-      dma_token(m + gstride, other, NDMA / 2, NDMA);
-      pend2 = false;
-    }
+    stage2(region, par, clr);
+    if (EARLY_X && it == 0 && !fwave) wait_vmcnt<0>();   // the next tile's x (issued by this I wave) has landed
     STAMP(sb + 4);
     lds_barrier();                                  // Bb: Y units complete
     STAMP(sb + 5);
