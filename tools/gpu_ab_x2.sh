@@ -1,3 +1,4 @@
+# (the bcfft_dm.hip switch this script measured was removed after its A/B; commit f61fd28 has it)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/x2 || exit 1
 for L in libbcfft_exp_x21.so libbcfft_exp_x22.so; do

@@ -1,3 +1,4 @@
+# (the bcfft_dm.hip switch this script measured was removed after its A/B; commit f61fd28 has it)
 # The symmetric P1 schedule (BCFFT_DM_SYM=1, libbcfft_exp_sym.so): DFT-kernel parity on that
 # library, then the interleaved fp32 headline A/B against the product.
 set -o pipefail
