@@ -40,6 +40,15 @@ def spectra(c: torch.Tensor, transpose_conj: bool = False) -> torch.Tensor:
     return out
 
 
+def _check_operand(t: torch.Tensor, device: torch.device, what: str, name: str) -> None:
+    """A spectra buffer or bias the kernels read by raw pointer must live on x's device, and a
+    spectra buffer must be contiguous (the library indexes it as the flat packed image)."""
+    if t.device != device:
+        raise ValueError(f"{what}: {name} is on {t.device} but x is on {device}; move it to x's device")
+    if name == "spectra" and not t.is_contiguous():
+        raise ValueError(f"{what}: the spectra buffer must be contiguous (use bcfft.ops.spectra's output as is)")
+
+
 def _check_spectra(spec: torch.Tensor, n_out: int, n_in: int, b: int, what: str) -> None:
     """The library cannot see the spectra buffer's size: a buffer built for another geometry
     would be read out of bounds. Checked here, before the launch."""
@@ -87,6 +96,7 @@ def forward_glu(x2d: torch.Tensor, spec_gu: torch.Tensor, block_size: int, gate_
     if block_size > 0 and gate_features % block_size == 0 and k % block_size == 0:
         _check_spectra(spec_gu, 32 * (-(-(gate_features // block_size) // 16)), k // block_size, block_size,
                        "bcfft.forward_glu")
+    _check_operand(spec_gu, x2d.device, "bcfft.forward_glu", "spectra")
     x2d = x2d.contiguous()
     if x2d.data_ptr() % 16:
         x2d = x2d.clone()
@@ -117,6 +127,8 @@ def forward_mlp(x2d: torch.Tensor, spec_gu: torch.Tensor, spec_down: torch.Tenso
     if b > 0 and k % b == 0 and inter_features % b == 0:
         _check_spectra(spec_gu, 32 * (-(-(inter_features // b) // 16)), k // b, b, "bcfft.forward_mlp")
         _check_spectra(spec_down, k // b, inter_features // b, b, "bcfft.forward_mlp")
+    _check_operand(spec_gu, x2d.device, "bcfft.forward_mlp", "spectra")
+    _check_operand(spec_down, x2d.device, "bcfft.forward_mlp", "spectra")
     x2d = x2d.contiguous()
     if x2d.data_ptr() % 16:
         x2d = x2d.clone()
@@ -220,6 +232,9 @@ def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, bl
     n, k = x2d.shape
     if block_size > 0 and out_features % block_size == 0 and k % block_size == 0:
         _check_spectra(spec, out_features // block_size, k // block_size, block_size, "bcfft.forward")
+    _check_operand(spec, x2d.device, "bcfft.forward", "spectra")
+    if bias is not None:
+        _check_operand(bias, x2d.device, "bcfft.forward", "bias")
     x2d = x2d.contiguous()
     if x2d.data_ptr() % 16:
         x2d = x2d.clone()

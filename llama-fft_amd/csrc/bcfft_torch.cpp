@@ -63,6 +63,15 @@ void check_spectra(const at::Tensor& spec, int64_t n_out, int64_t n_in, int64_t 
                     ") does not hold the (", n_out, ", ", n_in, ", ", b, ") operator (", need, " B)");
 }
 
+// a spectra buffer or bias read by raw pointer must live on x's device; a spectra buffer must be
+// contiguous (the library indexes the flat packed image) (bcfft/ops.py _check_operand)
+void check_operand(const at::Tensor& t, const at::Tensor& x, const char* what, const char* name, bool spectra) {
+  TORCH_CHECK_VALUE(t.device() == x.device(), what, ": ", name, " is on ", t.device(), " but x is on ", x.device(),
+                    "; move it to x's device");
+  TORCH_CHECK_VALUE(!spectra || t.is_contiguous(), what,
+                    ": the spectra buffer must be contiguous (use bcfft.ops.spectra's output as is)");
+}
+
 at::ScalarType out_dtype(const at::Tensor& x, const std::optional<at::Tensor>& bias) {
   return bias.has_value() ? at::promote_types(x.scalar_type(), bias->scalar_type()) : x.scalar_type();
 }
@@ -74,6 +83,8 @@ at::Tensor forward_hip(const at::Tensor& x, const at::Tensor& spec, const std::o
   const int64_t n = x.size(0), k = x.size(1);
   if (block_size > 0 && out_features % block_size == 0 && k % block_size == 0)
     check_spectra(spec, out_features / block_size, k / block_size, block_size, "bcfft.forward");
+  check_operand(spec, x, "bcfft.forward", "spectra", true);
+  if (bias.has_value()) check_operand(*bias, x, "bcfft.forward", "bias", false);
   const c10::DeviceGuard guard(x.device());
   const at::Tensor xa = aligned(x);
   at::Tensor y = at::empty({n, out_features}, x.options().dtype(out_dtype(x, bias)));
@@ -118,6 +129,7 @@ at::Tensor forward_glu_hip(const at::Tensor& x, const at::Tensor& spec_gu, int64
   if (block_size > 0 && gate_features % block_size == 0 && k % block_size == 0)
     check_spectra(spec_gu, 32 * ((gate_features / block_size + 15) / 16), k / block_size, block_size,
                   "bcfft.forward_glu");
+  check_operand(spec_gu, x, "bcfft.forward_glu", "spectra", true);
   const c10::DeviceGuard guard(x.device());
   const at::Tensor xa = aligned(x);
   at::Tensor h = at::empty({n, gate_features}, x.options());

@@ -82,3 +82,30 @@ def test_native_host_cost(dev, monkeypatch):
             modc = per_call(lambda: layer(x))
     print(f"host us/call: ops.forward native {nat:.1f} vs ctypes {cty:.1f}; module native {mod:.1f} vs ctypes {modc:.1f}")
     assert nat < cty * 1.1
+
+
+@pytest.mark.parametrize("native", [True, False])
+def test_operands_on_other_device_or_strided(dev, monkeypatch, native):
+    """A spectra buffer or bias on the host (or a strided spectra view) is refused before any
+    launch, with the same ValueError on the C++ and the ctypes path: the kernels read them by raw
+    device pointer."""
+    from bcfft import ops
+    g = torch.Generator(device="cpu").manual_seed(2)
+    c = (torch.randn(32, 32, 128, generator=g) * 0.01).to(dev)
+    spec = ops.spectra(c)
+    x = torch.randn(5, 4096, generator=g).to(dev)
+    with monkeypatch.context() as mp:
+        if not native:
+            _ctypes_path(mp)
+        with pytest.raises(ValueError, match="spectra is on cpu"):
+            ops.forward(x, spec.cpu(), None, 128, 4096)
+        with pytest.raises(ValueError, match="bias is on cpu"):
+            ops.forward(x, spec, torch.zeros(4096), 128, 4096)
+        wide = torch.zeros(2 * spec.numel(), device=dev)
+        wide[::2] = spec
+        with pytest.raises(ValueError, match="contiguous"):
+            ops.forward(x, wide[::2], None, 128, 4096)
+        sgu = ops.spectra(ops.glu_weights(c, c))
+        with pytest.raises(ValueError, match="spectra is on cpu"):
+            ops.forward_glu(x, sgu.cpu(), 128, 4096)
+        assert torch.equal(ops.forward(x, spec, None, 128, 4096), ops.forward(x, spec, None, 128, 4096))
