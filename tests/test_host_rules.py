@@ -76,3 +76,21 @@ def test_precise_mode_resolution(monkeypatch):
     assert not ops.glu_eligible(4096, 64, torch.float32, ops.resolve_algo(None, torch.float32, 64, 4096))
     monkeypatch.setenv("BCFFT_PRECISE", "0")
     assert ops.resolve_algo(None, torch.float32, 128, 4096) == "auto"
+
+
+def test_operand_device_and_layout_checks():
+    """bcfft.ops refuses a spectra buffer or bias that is not on x's device, and a strided spectra
+    view, before any launch (the C ABI reads them by raw device pointer; csrc/bcfft_torch.cpp
+    repeats the check for the C++ operators)."""
+    import torch
+    from bcfft import ops
+    dev = torch.device("cuda", 0)                 # x's device; the operands below live on the host
+    spec = torch.zeros(64)
+    with pytest.raises(ValueError, match="spectra is on cpu but x is on cuda:0"):
+        ops._check_operand(spec, dev, "bcfft.forward", "spectra")
+    with pytest.raises(ValueError, match="bias is on cpu"):
+        ops._check_operand(torch.zeros(8), dev, "bcfft.forward", "bias")
+    with pytest.raises(ValueError, match="contiguous"):
+        ops._check_operand(torch.zeros(128)[::2], torch.device("cpu"), "bcfft.forward", "spectra")
+    ops._check_operand(spec, torch.device("cpu"), "bcfft.forward", "spectra")
+    ops._check_operand(torch.zeros(16)[::2], torch.device("cpu"), "bcfft.forward", "bias")   # bias views are copied
