@@ -8,15 +8,15 @@ bench_all_in_one.py:484). A "step" = one forward over the rank's token shard.
 
 Multi-GPU: one process per GPU. `--gpus N` without a torch.distributed
 environment re-launches this script under `torch.distributed.run` with N ranks before any GPU
-call; with one (the driver's launch) WORLD_SIZE must equal --gpus. `--partition per-rank` (the
-default): every rank runs its own batch*seq = 8192-token shard of the job with no collective in
-the data path ("scaling": "weak": the layer is a per-token map, so the token axis shards with no
-exchange), and `value` = N x 8192 x M / the slowest rank's time. `--partition global` splits ONE
-8192-token batch into contiguous ceil(8192 / N)-row shards (1024 per rank at N = 8, SURVEY.md
-§8e's strong-scaling reading; "scaling": "strong"). With --allgather the
-single RCCL all-gather of the output shards (north star) is timed in a second loop: forward +
-all_gather_into_tensor, reported as `with_allgather` (gather-inclusive throughput) beside the
-sharded-compute `value`.
+call; with one (the driver's launch) WORLD_SIZE must equal --gpus. `--partition global` (the
+default, SURVEY.md §8e's contract): ONE batch*seq = 8192-token batch is split into contiguous
+ceil(8192 / N)-row shards (1024 per rank at N = 8; "scaling": "strong"), no collective in the data
+path, and `value` = 8192 x M / the slowest rank's time. At N > 1 the line also carries `weak`: the
+same ranks each running their own 8192-token batch (the per-rank reading, value = N x 8192 x M /
+the slowest rank's time); `--partition per-rank` makes that reading the headline instead. With
+--allgather the single RCCL all-gather of the output shards (north star) is timed in a second loop:
+forward + all_gather_into_tensor, reported as `with_allgather` (gather-inclusive throughput) beside
+the sharded-compute `value`.
 
 Prints ONE JSON line on rank 0. `roofline.achieved` = algorithmic bytes per launch
 (N*K*s_x + N*M*s_y + nO*nI*(b/2+1)*8 [+ M*s_bias]) / the kernel's average
@@ -464,9 +464,10 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--tokens", type=int, default=8192,
                     help="batch*seq: global tokens (--partition global) or tokens per rank (per-rank)")
-    ap.add_argument("--partition", default="per-rank", choices=("global", "per-rank"),
-                    help="global: shard the global tokens over the ranks (SURVEY.md §8e, strong scaling); "
-                         "per-rank: every rank runs --tokens (weak scaling)")
+    ap.add_argument("--partition", default="global", choices=("global", "per-rank"),
+                    help="global (default): shard the global tokens over the ranks (SURVEY.md §8e, strong "
+                         "scaling); per-rank: every rank runs --tokens (weak scaling; reported as `weak` "
+                         "beside a global headline at N > 1)")
     ap.add_argument("--in-features", type=int, default=4096)
     ap.add_argument("--out-features", type=int, default=4096)
     ap.add_argument("--block-size", type=int, default=128)
@@ -544,6 +545,18 @@ def main(argv=None):
     r = run_partitioned(fwd, x, n_total, args.steps, args.warmup, world, barrier, dev,
                         settle_ms=0.0 if stub else args.settle_ms, allgather=bool(args.allgather))
     wall, kern, reps = r["wall"], r["kern"], r["reps"]
+    weak = None
+    if world > 1 and args.partition == "global":     # the per-rank (weak-scaling) reading, same ranks
+        torch.manual_seed(1000 + rank)
+        xw = torch.randn(args.tokens, k, device=dev).to(DT[io])
+        rw = run_partitioned(fwd, xw, args.tokens * world, args.steps, args.warmup, world, barrier, dev,
+                             settle_ms=0.0, allgather=False, repeats=1)
+        weak = {"value": round(args.tokens * world * m / (rw["wall"] * 1e-3) / 1e9, 4),
+                "ms_per_step": round(rw["wall"], 5), "kernel_ms": round(rw["kern"], 5),
+                "tokens_per_rank": args.tokens, "scaling": "weak",
+                "note": "every rank runs its own batch*seq-token batch (no collective); value = all ranks' "
+                        "tokens x M / the slowest rank's time"}
+        del xw
     value = n_total * m / (wall * 1e-3) / 1e9
     nbytes = algo_bytes(n_local, k, m, b, io, bool(args.bias))
     gather = None
@@ -610,6 +623,8 @@ def main(argv=None):
                                     "shard runs the same kernel as N=1 on fewer tokens (1024 at N=8)")
         if gather:
             line["with_allgather"] = gather
+        if weak:
+            line["weak"] = weak
         if variants:
             line["variants"] = variants
         print(json.dumps(line), flush=True)

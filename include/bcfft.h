@@ -127,7 +127,9 @@ int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_feat
 /* The engine (enum bcfft_algo, AUTO resolved) that bcfft_forward_ws runs for these sizes and I/O
  * dtypes with the workspace bcfft_forward_workspace_bytes_io asks for; < 0 where it would refuse
  * the call. Host logic: nothing is launched. Replaces nothing in the reference (its forward has one
- * code path); benchmarks and tests use it to name what they time. */
+ * code path); benchmarks and tests use it to name what they time. BCFFT_ALGO_DFTP resolves to
+ * BCFFT_ALGO_DFTX unless x and y are both fp32 (the precise engine's only form); a 16-bit bias,
+ * which this query does not see, also runs DFTX. */
 int bcfft_forward_resolve(int64_t n_tokens, int in_features, int out_features, int block_size, int algo,
                           int x_dtype, int y_dtype);
 

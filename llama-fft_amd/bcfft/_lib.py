@@ -108,9 +108,11 @@ def load() -> ctypes.CDLL:
 def native_op() -> bool:
     """True once torch.ops.bcfft_native is loaded: the hot forward / forward_glu calls then go
     through one C++ dispatcher op (argument checks, allocation, stream lookup and the launch in
-    C++) instead of ctypes. False when that library is not built, when BCFFT_NATIVE_OP=0, or when
-    BCFFT_LIB_PATH names another engine library (the operators link the in-tree libbcfft.so).
-    Either way the kernels are libbcfft.so's: there is no CPU path."""
+    C++) instead of ctypes. False when that library is not built, when BCFFT_NATIVE_OP=0, when
+    BCFFT_LIB_PATH names another engine library (the operators link the in-tree libbcfft.so), or
+    when the library is present but does not load (e.g. built against another torch: undefined
+    c10 symbols), which warns once. Either way the kernels are libbcfft.so's (the ctypes path
+    calls the same ABI): there is no CPU path."""
     global _native
     if _native is None:
         with _lock:
@@ -118,8 +120,14 @@ def native_op() -> bool:
                 ok = (os.environ.get("BCFFT_NATIVE_OP", "1") != "0" and os.path.exists(TORCH_OP_PATH)
                       and os.path.basename(LIB_PATH) == "libbcfft.so")
                 if ok:
-                    load()                                    # the ABI version check first
-                    torch.ops.load_library(TORCH_OP_PATH)
+                    load()                                    # the ABI version check first (raises)
+                    try:
+                        torch.ops.load_library(TORCH_OP_PATH)
+                    except (OSError, RuntimeError) as e:      # stale / foreign build: the ctypes path
+                        import warnings
+                        warnings.warn(f"{TORCH_OP_PATH} did not load ({e}); bcfft calls libbcfft.so through "
+                                      "ctypes instead. Rebuild with `make -C llama-fft_amd`.", RuntimeWarning)
+                        ok = False
                 _native = ok
     return _native
 

@@ -8,6 +8,7 @@
 //   BlockCirculantLinear.forward: reference src/patch_llama_fft.py:226-275
 //   fused gate/up + SwiGLU:        reference src/patch_llama_fft.py:343-394
 #include <ATen/ATen.h>
+#include <ATen/core/dispatch/Dispatcher.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
@@ -98,10 +99,27 @@ at::Tensor forward_hip(const at::Tensor& x, const at::Tensor& spec, const std::o
     bcode = dtype_code(ba.scalar_type());
   }
   const int xc = dtype_code(xa.scalar_type()), yc = dtype_code(y.scalar_type());
-  // split-K workspace (short grids of the MFMA and streamed-weight kernels) from torch's allocator
-  int64_t ws_bytes = split_k ? bcfft_forward_workspace_bytes_io(n, (int)k, (int)out_features, (int)block_size,
-                                                                (int)algo, xc, yc)
-                             : 0;
+  // split-K workspace (short grids of the MFMA and streamed-weight kernels) from torch's allocator;
+  // the query is host logic keyed by the geometry, so a layer called again with the same shape
+  // (every decode step, every prefill batch of one size) reuses the last answer
+  struct WsKey {
+    int64_t n, k, o, b, algo;
+    int xc, yc;
+    bool operator==(const WsKey& r) const {
+      return n == r.n && k == r.k && o == r.o && b == r.b && algo == r.algo && xc == r.xc && yc == r.yc;
+    }
+  };
+  thread_local WsKey ws_key{-1, 0, 0, 0, 0, 0, 0};
+  thread_local int64_t ws_cached = 0;
+  int64_t ws_bytes = 0;
+  if (split_k) {
+    const WsKey key{n, k, out_features, block_size, algo, xc, yc};
+    if (!(key == ws_key)) {
+      ws_cached = bcfft_forward_workspace_bytes_io(n, (int)k, (int)out_features, (int)block_size, (int)algo, xc, yc);
+      ws_key = key;
+    }
+    ws_bytes = ws_cached;
+  }
   at::Tensor ws;
   if (ws_bytes > 0) ws = at::empty({ws_bytes}, x.options().dtype(at::kByte));
   else ws_bytes = 0;
@@ -160,6 +178,37 @@ at::Tensor forward_glu_cpu(const at::Tensor& x, const at::Tensor&, int64_t, int6
   return x;
 }
 
+// Autograd key: these operators are forward-only (the module's backward is bcfft.ops' custom
+// autograd Function over the same kernels, patch_llama_fft._BCFunction). Called directly with an
+// input that requires grad under grad mode, they refuse instead of returning a tensor without a
+// grad_fn (which would only warn at backward time); otherwise they dispatch below autograd.
+bool wants_grad(const at::Tensor& t) { return t.defined() && t.requires_grad(); }
+
+at::Tensor forward_autograd(const at::Tensor& x, const at::Tensor& spec, const std::optional<at::Tensor>& bias,
+                            int64_t block_size, int64_t out_features, int64_t algo, bool split_k) {
+  TORCH_CHECK(!(at::GradMode::is_enabled() && (wants_grad(x) || wants_grad(spec) || (bias && wants_grad(*bias)))),
+              "torch.ops.bcfft_native.forward is forward-only: call it under torch.no_grad() / inference_mode, "
+              "or use BlockCirculantLinear / bcfft.ops.forward, whose autograd Function has the backward");
+  at::AutoDispatchBelowADInplaceOrView guard;
+  static auto op = c10::Dispatcher::singleton()
+                       .findSchemaOrThrow("bcfft_native::forward", "")
+                       .typed<at::Tensor(const at::Tensor&, const at::Tensor&, const std::optional<at::Tensor>&,
+                                         int64_t, int64_t, int64_t, bool)>();
+  return op.call(x, spec, bias, block_size, out_features, algo, split_k);
+}
+
+at::Tensor forward_glu_autograd(const at::Tensor& x, const at::Tensor& spec_gu, int64_t block_size,
+                                int64_t gate_features, int64_t algo) {
+  TORCH_CHECK(!(at::GradMode::is_enabled() && (wants_grad(x) || wants_grad(spec_gu))),
+              "torch.ops.bcfft_native.forward_glu is forward-only: call it under torch.no_grad() / "
+              "inference_mode (the fused gate/up serves inference)");
+  at::AutoDispatchBelowADInplaceOrView guard;
+  static auto op = c10::Dispatcher::singleton()
+                       .findSchemaOrThrow("bcfft_native::forward_glu", "")
+                       .typed<at::Tensor(const at::Tensor&, const at::Tensor&, int64_t, int64_t, int64_t)>();
+  return op.call(x, spec_gu, block_size, gate_features, algo);
+}
+
 }  // namespace
 
 TORCH_LIBRARY(bcfft_native, m) {
@@ -181,4 +230,9 @@ TORCH_LIBRARY_IMPL(bcfft_native, Meta, m) {
 TORCH_LIBRARY_IMPL(bcfft_native, CPU, m) {
   m.impl("forward", &forward_cpu);
   m.impl("forward_glu", &forward_glu_cpu);
+}
+
+TORCH_LIBRARY_IMPL(bcfft_native, Autograd, m) {
+  m.impl("forward", &forward_autograd);
+  m.impl("forward_glu", &forward_glu_autograd);
 }

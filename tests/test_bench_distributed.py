@@ -31,18 +31,28 @@ def _line(out):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("partition,per_rank,total,scaling", [("global", 100, 200, "strong"),
+@pytest.mark.parametrize("partition,per_rank,total,scaling", [(None, 100, 200, "strong"),
+                                                              ("global", 100, 200, "strong"),
                                                               ("per-rank", 200, 400, "weak")])
 def test_gpus2_launches_two_ranks(partition, per_rank, total, scaling):
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--partition", partition,
+    """partition None: the default, which must be SURVEY.md §8e's global split (strong scaling), with
+    the per-rank (weak) reading beside it under `weak`."""
+    part = [] if partition is None else ["--partition", partition]
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *part,
                           *ARGS], capture_output=True, text=True, timeout=300, env=_env())
     assert out.returncode == 0, out.stderr[-3000:]
     d = _line(out.stdout)
     assert d["n_gpus"] == 2 and d["scaling"] == scaling
+    assert d["config"]["partition"] == (partition or "global")
     assert d["config"]["tokens_per_rank"] == per_rank and d["config"]["global_tokens"] == total
     assert d["value"] > 0 and d["ms_per_step"] > 0
     g = d["with_allgather"]
     assert g["ms_per_step"] >= d["ms_per_step"] * 0.5 and g["value"] > 0
+    if scaling == "strong":
+        w = d["weak"]
+        assert w["scaling"] == "weak" and w["tokens_per_rank"] == 200 and w["value"] > 0
+    else:
+        assert "weak" not in d
 
 
 def test_gpus4_global_partition():

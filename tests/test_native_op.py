@@ -38,3 +38,18 @@ def test_native_op_host_tensors_fail_loudly():
         ops.forward_glu(torch.zeros(3, 4096), torch.zeros(8), 128, 4096, 0)
     with pytest.raises(RuntimeError, match="no CPU path"):      # bcfft.ops with the native op loaded
         bcfft.ops.forward(torch.zeros(3, 4096), torch.zeros(8), None, 128, 4096)
+
+
+def test_broken_native_library_falls_back_to_ctypes(tmp_path, monkeypatch):
+    """A libbcfft_torch.so that exists but does not load (stale build against another torch, a
+    truncated file) must not take the forward path down: one warning, then the ctypes binding of
+    the same libbcfft.so. Host tensors still fail loudly there."""
+    bogus = tmp_path / "libbcfft_torch.so"
+    bogus.write_bytes(b"not an ELF object")
+    monkeypatch.setattr(_lib, "TORCH_OP_PATH", str(bogus))
+    monkeypatch.setattr(_lib, "_native", None)
+    with pytest.warns(RuntimeWarning, match="did not load"):
+        assert _lib.native_op() is False
+    assert _lib.native_op() is False                         # decided once, no second warning
+    with pytest.raises(RuntimeError, match="no CPU path"):  # bcfft.ops on the ctypes path
+        bcfft.ops.forward(torch.zeros(3, 4096), torch.zeros(8), None, 128, 4096)
