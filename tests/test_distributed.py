@@ -78,3 +78,40 @@ def test_shard_bounds_cover_exactly():
                 assert bnd == c2 and a <= bnd
     with pytest.raises(ValueError):
         shard_bounds(10, 2, 2)
+
+
+def _logits_worker(rank, world, port, n_prompts, vocab, q):
+    """model_bench's config-5 collective on gloo: each rank holds the last-token logits of its
+    prompt slice (bc_eval.prompt_shard), gather_prompt_logits reassembles them in prompt order."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import bc_eval as E
+        import model_bench as MB
+        prompts = list(range(n_prompts))                    # stand-ins: prompt i's logits row is i
+        mine = E.prompt_shard(prompts, world, rank)
+        last = torch.stack([torch.full((vocab,), float(p)) for p in mine]) if mine else torch.zeros(0, vocab)
+        q.put((rank, MB.gather_prompt_logits(last, n_prompts).numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_prompts", [100, 7])
+def test_model_bench_logits_gather_gloo_world2(n_prompts):
+    """tools/model_bench.py's distributed branch (BASELINE config 5: prompt replicas + ONE all-gather
+    of last-token logits, bench_all_in_one.py:348-389) with two gloo ranks on the CPU."""
+    world, vocab = 2, 16
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_logits_worker, args=(r, world, port, n_prompts, vocab, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = np.repeat(np.arange(n_prompts, dtype=np.float32)[:, None], vocab, 1)
+    for _, rows in res:
+        np.testing.assert_array_equal(rows, want)

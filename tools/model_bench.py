@@ -112,6 +112,17 @@ def decode(model, batches, new_tokens, pad_id):
     return sync_max(time.perf_counter() - t0)
 
 
+def gather_prompt_logits(last: torch.Tensor, n_prompts: int, group=None) -> torch.Tensor:
+    """Config 5's one collective (bench_all_in_one.py:348-389 scores every prompt's last-token
+    logits): this rank's (its prompt slice, V) logits to every rank, reassembled in prompt order.
+    The slices are bc_eval.prompt_shard's contiguous shard_bounds, as gather_rows expects; RCCL
+    all_gather_into_tensor on GPU ranks, gloo's list all-gather in the CPU test."""
+    from bcfft.shard import gather_rows
+    rows = gather_rows(last.contiguous(), n_prompts, group)
+    assert rows.shape[0] == n_prompts
+    return rows
+
+
 def _keep(store, key, pick):
     """A hook that records pick(...) under key once and returns None (a forward hook's return
     value would replace the module's output)."""
@@ -206,10 +217,17 @@ def main(argv=None):
     ap.add_argument("--temperature", type=float, default=1.0)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--config-overrides", default="{}", help="JSON LlamaConfig overrides (tests)")
+    ap.add_argument("--dump-logits", default="",
+                    help="rank 0 saves the student's last-token logits of ALL prompts (after the all-gather "
+                         "when distributed) and the teacher's local ones to this .pt file (tests)")
     args = ap.parse_args(argv)
     block_sizes = [int(b) for b in args.block_sizes.split(",") if b.strip()]
 
     import patch_llama_fft as P
+    # under torch.distributed.run (WORLD_SIZE set, any world size, 1 included) the RCCL group is
+    # created with device_id before the GPU is touched, and every collective below keys on
+    # dist.is_initialized(): the config-5 path runs whenever a launcher started this process
+    launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -217,7 +235,8 @@ def main(argv=None):
         raise SystemExit("model_bench needs a ROCm GPU (the BC engine has no CPU path)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    own_pg = launched and not dist.is_initialized()
+    if own_pg:
         dist.init_process_group("nccl", device_id=dev)
 
     if args.prompts < world:
@@ -229,7 +248,7 @@ def main(argv=None):
     batches = [tuple(t.to(dev) for t in b) for b in E.iter_batches(mine, args.batch_size, cfg.pad_token_id)]
     my_tokens = sum(int(a.sum()) for _, a in mine)
     tok = torch.tensor([my_tokens], device=dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.all_reduce(tok)
     total_tokens = int(tok.item())
     n_patch = cfg.num_hidden_layers if args.num_layers < 0 else args.num_layers
@@ -266,14 +285,16 @@ def main(argv=None):
 
         # config 5's single collective: every rank's last-token logits to every rank (RCCL). The
         # prompt shards are shard_bounds' contiguous slices, so gather_rows reassembles them in order.
-        if world > 1:
-            from bcfft.shard import gather_rows
+        all_last = student_last
+        if dist.is_initialized():
             barrier()
             tg = time.perf_counter()
-            rows = gather_rows(student_last.contiguous(), args.prompts)
+            all_last = gather_prompt_logits(student_last, args.prompts)
             barrier()
             res["allgather_logits_s"] = sync_max(time.perf_counter() - tg)
-            assert rows.shape[0] == args.prompts
+        if args.dump_logits and rank == 0 and bi == 0:
+            torch.save({"student_last": all_last.cpu(), "teacher_last_local": teacher_last.cpu(),
+                        "world": world}, args.dump_logits)
 
         if rank == 0:
             n_prompts_new = args.prompts * args.new_tokens
@@ -307,7 +328,7 @@ def main(argv=None):
                 line["allgather_logits_ms"] = round(res["allgather_logits_s"] * 1e3, 3)
                 line["value_with_allgather"] = round(total_tokens / (t_bc + res["allgather_logits_s"]), 1)
             print(json.dumps(line), flush=True)
-    if world > 1:
+    if own_pg:
         dist.destroy_process_group()
     return line if rank == 0 else None
 
