@@ -71,10 +71,12 @@ MAC = {
     "bc_forward_dm256k_kernel": "MFMA fp16 throughout, b=256 as three 128-point virtual rows, 16-block K-chunks with "
                                 "weight fragments streamed from L2 (bf16 I/O)",
     "bc_forward_stat_kernel": "MFMA fp16: conj(C)*s_o (VGPR-resident) x per-token-scaled X split hi+lo, f32 accumulate",
+    "bc_forward_sn_kernel": "MFMA fp16 throughout (short-N: one workgroup per 4-token tile and 16 output blocks), "
+                            "a/d, X and Y hi+lo, f32 accumulate",
     "bc_forward_mfma_kernel": "MFMA bf16 hi/lo split (Xhi+Xlo)(Chi+Clo), f32 accumulate",
     "bc_forward_valu_kernel": "VALU fp32 FMA",
 }
-ALGO_NAMES = {0: "auto", 1: "mfma", 2: "valu", 3: "stationary", 4: "dft", 5: "dftx", 6: "dftp"}
+ALGO_NAMES = {0: "auto", 1: "mfma", 2: "valu", 3: "stationary", 4: "dft", 5: "dftx", 6: "dftp", 7: "short"}
 
 
 def resolved_kernel(algo, k, b, io="fp32", m=4096, n=8192):

@@ -62,7 +62,11 @@ enum bcfft_dtype { BCFFT_NONE = -1, BCFFT_F32 = 0, BCFFT_F16 = 1, BCFFT_BF16 = 2
  *        DFT on its other geometries; else STAT where eligible, else MFMA for block_size <= 128,
  *        else VALU. */
 enum bcfft_algo { BCFFT_ALGO_AUTO = 0, BCFFT_ALGO_MFMA = 1, BCFFT_ALGO_VALU = 2, BCFFT_ALGO_STAT = 3,
-                  BCFFT_ALGO_DFT = 4, BCFFT_ALGO_DFTX = 5, BCFFT_ALGO_DFTP = 6 };
+                  BCFFT_ALGO_DFT = 4, BCFFT_ALGO_DFTX = 5, BCFFT_ALGO_DFTP = 6, BCFFT_ALGO_SHORT = 7 };
+/* BCFFT_ALGO_SHORT: the short-N DFT kernel (one workgroup per 4-token tile and 16 output blocks,
+ * the exact hi + lo arithmetic of DFTX) for the STAT geometries (b = 128 with K = 4096; b = 64 with
+ * K = 2048 or 4096). AUTO takes it for those geometries at token counts whose persistent-kernel
+ * grid would leave most CUs idle (decode steps, BASELINE config 1). */
 
 enum bcfft_status {
   BCFFT_OK = 0,

@@ -17,9 +17,9 @@ LIB_PATH = os.environ.get("BCFFT_LIB_PATH") or os.path.join(os.path.dirname(_HER
 ABI_VERSION = 1
 
 BCFFT_NONE, BCFFT_F32, BCFFT_F16, BCFFT_BF16 = -1, 0, 1, 2
-ALGO_AUTO, ALGO_MFMA, ALGO_VALU, ALGO_STAT, ALGO_DFT, ALGO_DFTX, ALGO_DFTP = 0, 1, 2, 3, 4, 5, 6
+ALGO_AUTO, ALGO_MFMA, ALGO_VALU, ALGO_STAT, ALGO_DFT, ALGO_DFTX, ALGO_DFTP, ALGO_SHORT = 0, 1, 2, 3, 4, 5, 6, 7
 ALGOS = {"auto": ALGO_AUTO, "mfma": ALGO_MFMA, "valu": ALGO_VALU, "stationary": ALGO_STAT, "dft": ALGO_DFT,
-         "dftx": ALGO_DFTX, "dftp": ALGO_DFTP}
+         "dftx": ALGO_DFTX, "dftp": ALGO_DFTP, "short": ALGO_SHORT}
 DTYPE_CODE = {torch.float32: BCFFT_F32, torch.float16: BCFFT_F16, torch.bfloat16: BCFFT_BF16}
 SUPPORTED_BLOCKS = (32, 64, 128, 256)
 MLP_MODES = {"auto": 0, "fused": 1, "split": 2, "fused_splitk": 3}

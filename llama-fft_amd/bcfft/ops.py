@@ -166,10 +166,10 @@ def glu_eligible(in_features: int, block_size: int, dtype: torch.dtype | None = 
     callers fall back to two launches instead of meeting BCFFT_ERR_BLOCK. Mirrors the C rules:
     b = 256 with K = 4096 only for bf16 x under auto / dft, up to 512 gate blocks (the kernel's
     group limit); otherwise the stationary geometries, where dftx needs b = 128 with K = 4096 and
-    dft that or b = 64 with K = 4096 and bf16 x; mfma / valu have no fused form. algo None: the
+    dft that or b = 64 with K = 4096 and bf16 x; mfma / valu / short have no fused form. algo None: the
     BCFFT_ALGO environment (default auto)."""
     algo = default_algo() if algo is None else algo
-    if algo in ("mfma", "valu") or block_size <= 0 or in_features % block_size:
+    if algo in ("mfma", "valu", "short") or block_size <= 0 or in_features % block_size:
         return False
     n_in = in_features // block_size
     if block_size == 256 and n_in == 16:

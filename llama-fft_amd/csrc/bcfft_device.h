@@ -601,6 +601,18 @@ bool launch_forward_glu(int b, int n_in, int xdt, const void* x, int64_t n, int 
 void launch_stat_image(int b, int n_out, int n_in, void* spec, hipStream_t s);
 // the precise engine's e4m3 weight residual image (b = 128, K = 4096; after launch_stat_image)
 void launch_lo8_image(int n_out, void* spec, hipStream_t s);
+// short-N DFT kernel (bcfft_sn.hip): the STAT image's geometries, one workgroup per 4-token tile
+// and 16-wide N-tile, one workgroup per CU (LDS). AUTO takes it while those workgroups fit one
+// round on the device (sn_pays): measured against the persistent engines (tools/time_algos.py
+// --short, profiles/r05e_time_short.log) it wins through one round and loses from two (e.g.
+// 4096 -> 4096 b = 128 fp32: 9.9 vs 11.3 us at N = 512 = 256 workgroups, 19.6 vs 14.1 at 1024)
+bool sn_eligible(int n_in, int b);
+bool launch_forward_sn(int b, int n_in, int xdt, bool yf32, const void* x, int64_t n, int n_out, const void* spec,
+                       const void* bias, int bias_dt, void* y, hipStream_t s);
+inline int64_t sn_workgroups(int64_t n_tokens, int n_out) { return (n_tokens + 3) / 4 * ((n_out + 15) / 16); }
+inline bool sn_pays(int64_t n_tokens, int n_out) {
+  return n_tokens > 0 && sn_workgroups(n_tokens, n_out) <= device_cu_count();
+}
 // DFT-on-MFMA kernel (bcfft_dm.hip): the STAT image's geometry subset b = 128, K = 4096
 bool dm_eligible(int n_in, int b);
 bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, int mode, const void* x, int64_t n, int n_out,

@@ -593,6 +593,7 @@ const char* algo_name(int a) {
     case BCFFT_ALGO_DFT: return "dft";
     case BCFFT_ALGO_DFTX: return "dftx";
     case BCFFT_ALGO_DFTP: return "dftp";
+    case BCFFT_ALGO_SHORT: return "short";
     default: return "?";
   }
 }
@@ -765,8 +766,13 @@ int bcfft_spectra(const void* c, int c_dtype, int n_out_blocks, int n_in_blocks,
 // fp32 outputs take DFTX at b = 128 (its hi + lo products keep the layer linear in x to ~1e-6,
 // which fp32 training gradients through dx rely on); 16-bit outputs take the one-term DFT, whose
 // noise sits far below their own rounding.
-static int resolve_algo(int algo, int n_in, int block_size, int xdt = -2, bool yf32 = true, int64_t n_tokens = -1) {
+static int resolve_algo(int algo, int n_in, int block_size, int xdt = -2, bool yf32 = true, int64_t n_tokens = -1,
+                        int n_out = 0) {
   if (algo != BCFFT_ALGO_AUTO) return algo;
+  // short token counts on the STAT geometries: one workgroup per (4-token tile, 16 output blocks)
+  // instead of a persistent grid of ceil(N / 4) x groups workgroups (bcfft_sn.hip)
+  if (n_tokens >= 0 && n_out > 0 && bcfft::sn_eligible(n_in, block_size) && bcfft::sn_pays(n_tokens, n_out))
+    return BCFFT_ALGO_SHORT;
   if (bcfft::dm_eligible(n_in, block_size)) return yf32 ? BCFFT_ALGO_DFTX : BCFFT_ALGO_DFT;
   if (bcfft::dm64_eligible(n_in, block_size, xdt, yf32)) return BCFFT_ALGO_DFT;
 #ifndef BCFFT_NO_DM256
@@ -788,14 +794,16 @@ static int64_t ws_bytes_for(int64_t n_tokens, int in_features, int out_features,
       in_features % block_size || out_features % block_size)
     return -1;
   const int n_in = in_features / block_size;
-  const int a = resolve_algo(algo, n_in, block_size, xdt, yf32, n_tokens);
+  const int a = resolve_algo(algo, n_in, block_size, xdt, yf32, n_tokens, out_features / block_size);
   // the DFT engines take no workspace, except the down projection's streamed-weight kernel at
   // short grids (its K-chunk split: kz fp32 partial slabs)
   if (a == BCFFT_ALGO_DFT && bcfft::dmk_eligible(in_features / block_size, block_size, xdt, yf32)) {
     const int kz = bcfft::dmk_ksplit(n_tokens, in_features / block_size, out_features / block_size);
     return kz < 2 ? 0 : kz * n_tokens * (int64_t)out_features * (int64_t)sizeof(float);
   }
-  if (a == BCFFT_ALGO_DFT || a == BCFFT_ALGO_DFTX || a == BCFFT_ALGO_DFTP || a == BCFFT_ALGO_STAT) return 0;
+  if (a == BCFFT_ALGO_DFT || a == BCFFT_ALGO_DFTX || a == BCFFT_ALGO_DFTP || a == BCFFT_ALGO_STAT ||
+      a == BCFFT_ALGO_SHORT)
+    return 0;
   int kz = 1;
   if (a == BCFFT_ALGO_MFMA && block_size <= BCFFT_MFMA_MAXB) kz = mfma_ksplit(n_tokens, n_in, block_size);
   else if (a == BCFFT_ALGO_VALU || a == BCFFT_ALGO_MFMA) kz = valu_ksplit(n_tokens, n_in, block_size);
@@ -827,7 +835,7 @@ int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_featur
     return BCFFT_ERR_DTYPE;
   if (y_dtype != promote(x_dtype, bias_dtype)) return BCFFT_ERR_DTYPE;
   if ((bias == nullptr) != (bias_dtype == BCFFT_NONE)) return BCFFT_ERR_ARG;
-  if (algo < BCFFT_ALGO_AUTO || algo > BCFFT_ALGO_DFTP) return BCFFT_ERR_ARG;
+  if (algo < BCFFT_ALGO_AUTO || algo > BCFFT_ALGO_SHORT) return BCFFT_ERR_ARG;
   if (n_tokens == 0) return BCFFT_OK;
   if (!x || !y || !spectra) return BCFFT_ERR_ARG;
   if (!aligned16(x) || !aligned16(y) || !aligned16(spectra) || (bias && !aligned16(bias)) ||
@@ -836,6 +844,8 @@ int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_featur
   const int n_in = in_features / block_size, n_out = out_features / block_size;
   const bool stat_ok = bcfft::stat_eligible(n_in, block_size);
   if (algo == BCFFT_ALGO_STAT && !stat_ok) return refuse("bcfft_forward", algo, n_in, block_size, x_dtype, y_dtype);
+  if (algo == BCFFT_ALGO_SHORT && !bcfft::sn_eligible(n_in, block_size))
+    return refuse("bcfft_forward", algo, n_in, block_size, x_dtype, y_dtype);
   const bool dm64 = bcfft::dm64_eligible(n_in, block_size, x_dtype, y_dtype == BCFFT_F32);
   if ((algo == BCFFT_ALGO_DFTX || algo == BCFFT_ALGO_DFTP) && !bcfft::dm_eligible(n_in, block_size))
     return refuse("bcfft_forward", algo, n_in, block_size, x_dtype, y_dtype);
@@ -844,12 +854,17 @@ int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_featur
   const bool dm64k = bcfft::dm64k_eligible(n_in, block_size, x_dtype, y_dtype == BCFFT_F32);
   if (algo == BCFFT_ALGO_DFT && !bcfft::dm_eligible(n_in, block_size) && !dm64 && !dmk && !dm256 && !dm64k)
     return refuse("bcfft_forward", algo, n_in, block_size, x_dtype, y_dtype);
-  algo = resolve_algo(algo, n_in, block_size, x_dtype, y_dtype == BCFFT_F32, n_tokens);
+  algo = resolve_algo(algo, n_in, block_size, x_dtype, y_dtype == BCFFT_F32, n_tokens, n_out);
   // the workspace is used only when it is as large as bcfft_forward_workspace_bytes_io asks
   const int64_t need = ws_bytes_for(n_tokens, in_features, out_features, block_size, algo, x_dtype,
                                        y_dtype == BCFFT_F32);
   float* ws = (workspace && need > 0 && workspace_bytes >= need) ? (float*)workspace : nullptr;
   hipStream_t s = (hipStream_t)stream;
+  if (algo == BCFFT_ALGO_SHORT) {
+    bcfft::launch_forward_sn(block_size, n_in, x_dtype, y_dtype == BCFFT_F32, x, n_tokens, n_out, spectra, bias,
+                             bias_dtype, y, s);
+    return record_launch();
+  }
   if (algo == BCFFT_ALGO_DFT && dmk) {
     if (ws) bcfft::launch_forward_dmk_split(x, n_tokens, n_in, n_out, spectra, bias, bias_dtype, y, ws,
                                             bcfft::dmk_ksplit(n_tokens, n_in, n_out), s);
@@ -898,7 +913,7 @@ static int forward_plan(int64_t n_tokens, int in_features, int out_features, int
       in_features % block_size || out_features % block_size)
     return -1;
   if (!valid_dt(x_dtype) || !valid_dt(y_dtype)) return -1;
-  if (algo < BCFFT_ALGO_AUTO || algo > BCFFT_ALGO_DFTP) return -1;
+  if (algo < BCFFT_ALGO_AUTO || algo > BCFFT_ALGO_SHORT) return -1;
   const int n_in = in_features / block_size, n_out = out_features / block_size;
   const bool yf32 = y_dtype == BCFFT_F32;
   const bool dm = bcfft::dm_eligible(n_in, block_size);
@@ -907,13 +922,15 @@ static int forward_plan(int64_t n_tokens, int in_features, int out_features, int
   const bool dm256 = bcfft::dm256_eligible(n_in, block_size, x_dtype, yf32);
   const bool dm64k = bcfft::dm64k_eligible(n_in, block_size, x_dtype, yf32);
   if (algo == BCFFT_ALGO_STAT && !bcfft::stat_eligible(n_in, block_size)) return -1;
+  if (algo == BCFFT_ALGO_SHORT && !bcfft::sn_eligible(n_in, block_size)) return -1;
   if ((algo == BCFFT_ALGO_DFTX || algo == BCFFT_ALGO_DFTP) && !dm) return -1;
   if (algo == BCFFT_ALGO_DFT && !dm && !dm64 && !dmk && !dm256 && !dm64k) return -1;
-  int a = resolve_algo(algo, n_in, block_size, x_dtype, yf32, n_tokens);
+  int a = resolve_algo(algo, n_in, block_size, x_dtype, yf32, n_tokens, n_out);
   // the precise engine serves fp32 x with fp32 outputs only; launch_forward_dm runs DFTX for 16-bit x
   // or outputs (and for a 16-bit bias on fp32 x, which this query does not see: bcfft.h)
   if (a == BCFFT_ALGO_DFTP && !(x_dtype == BCFFT_F32 && yf32)) a = BCFFT_ALGO_DFTX;
-  if (a == BCFFT_ALGO_DFT && dmk) *kernel = "bc_forward_dmk_kernel";
+  if (a == BCFFT_ALGO_SHORT) *kernel = "bc_forward_sn_kernel";
+  else if (a == BCFFT_ALGO_DFT && dmk) *kernel = "bc_forward_dmk_kernel";
   else if (a == BCFFT_ALGO_DFT && dm256) *kernel = bcfft::dm256_kernel_name(n_tokens, n_in, n_out);
   else if (a == BCFFT_ALGO_DFT && dm64k) *kernel = "bc_forward_dm64k_kernel";
   else if (a == BCFFT_ALGO_DFT && block_size == 64)

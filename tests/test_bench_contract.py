@@ -34,7 +34,15 @@ def test_engine_resolution_mirrors_auto_rule(built_lib):
     assert bench.resolved_kernel("auto", 2048, 64, "bf16")[1] == "bc_forward_stat_kernel"
     assert bench.resolved_kernel("valu", 4096, 128)[1] == "bc_forward_valu_kernel"
     assert bench.resolved_kernel("auto", 4096, 128, "bf16", 11008, 8192)[1] == "bc_forward_dmg_kernel"
-    assert bench.resolved_kernel("auto", 4096, 128, "bf16", 11008, 20)[1] == "bc_forward_dm8_kernel"  # short grid
+    # short token counts on the STAT geometries: the short-N kernel (bcfft_sn.hip), e.g. a decode step
+    # and BASELINE config 1; the persistent engines from BCFFT_SN_MAX_TOKENS + 1 tokens
+    assert bench.resolved_kernel("auto", 4096, 128, "bf16", 11008, 20)[:2] == ("short", "bc_forward_sn_kernel")
+    assert bench.resolved_kernel("auto", 4096, 64, "fp32", 4096, 128)[:2] == ("short", "bc_forward_sn_kernel")
+    assert bench.resolved_kernel("auto", 4096, 128, "fp32", 4096, 1)[1] == "bc_forward_sn_kernel"
+    assert bench.resolved_kernel("auto", 4096, 128, "fp32", 4096, 8192)[1] == "bc_forward_dm_kernel"
+    assert bench.resolved_kernel("short", 4096, 128, "fp32", 4096, 8192)[1] == "bc_forward_sn_kernel"
+    with pytest.raises(ValueError):
+        bench.resolved_kernel("short", 11008, 128, "bf16")   # not a STAT geometry
     assert bench.resolved_kernel("auto", 11008, 128, "bf16", 4096, 8192)[1] == "bc_forward_dmk_kernel"
     assert bench.resolved_kernel("auto", 11008, 64, "bf16", 4096, 8192)[1] == "bc_forward_dm64k_kernel"
     assert bench.resolved_kernel("auto", 11008, 64, "bf16", 4096, 64)[1] == "bc_forward_mfma_kernel"  # < 128 tokens

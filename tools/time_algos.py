@@ -92,6 +92,10 @@ if __name__ == "__main__":
                   (4096, 11008, 256, "bf16", 1700), (11008, 4096, 256, "bf16", 1024), (11008, 4096, 256, "bf16", 64)]
     if "--down2" in sys.argv:
         shapes = [(11008, 4096, 128, "bf16", n) for n in (1700, 8192)]
+    if "--short" in sys.argv:                       # the short-N kernel against the persistent engines
+        shapes = ([(4096, 4096, 64, "fp32", n) for n in (1, 16, 64, 128, 256, 512, 1024)]
+                  + [(4096, 4096, 128, io, n) for io in ("fp32", "bf16") for n in (1, 16, 64, 128, 256, 512, 1024)]
+                  + [(4096, 11008, 128, "bf16", n) for n in (20, 128, 256, 512)])
     if "--smalln" in sys.argv:                      # AUTO's small-N crossover
         shapes = [(4096, 4096, b, io, n) for b in (64, 128) for io in ("fp32",) for n in (16, 64, 128, 256, 512, 1024, 2048)]
     for k, m, b, io, n in shapes:

@@ -33,7 +33,7 @@ def main():
     out = {}
     for n in (128, 256, 1024):
         x = torch.randn(n, k, device="cuda")
-        for algo in ("auto", "stationary", "mfma", "valu"):
+        for algo in ("auto", "short", "stationary", "mfma", "valu"):
             f = lambda t, a=algo: ops.forward(t, spec, None, b, m, algo=a)  # noqa: E731
             with torch.inference_mode():
                 e = timed(lambda: f(x), 100, 1)
