@@ -14,17 +14,19 @@
 //    the x DMA, stage 1 and stage 3 (so no barrier is needed between its stage 3 and the DMA
 //    into the same slots), and bins 4w .. 4w + 3 in stage 2 for all 16 tokens.
 //  * One step per (tile, chunk): [tile's first chunk: stage 3 of the previous tile's tokens w,
-//    w + 8] -> x DMA of the next step's chunk into the other region -> stage 1 | Ba | stage 2 |
-//    Bb | [last chunk: Y of the 16 tokens into the chunk's region | Be].
+//    w + 8] -> stage 1 (issuing, per token, the x DMA of the next step's chunk into the other
+//    region) | Ba | stage 2 | Bb | [last chunk: Y of the 16 tokens into the chunk's region | Be].
+//  * Stage 1 on raw bf16 x: the 64-point transform as bf16 MFMAs against F 2^-7 in bf16 hi + lo
+//    (round 5; the even / odd fp16 form before it is kept under BCFFT_DM64K_F16S1 for A/B).
 //  * Numerics: per-(token, 16-block quarter) power-of-two scales from stage 1 with HEAD bits of
 //    headroom; stage 2 aligns each quarter to the token's running reference exponent (an exact
 //    fp16 power of two on the A rows) and scales the accumulator rows down once when a chunk is
 //    more than 2^HEAD louder (bcfft_dmk.hip's scheme). |X| <= 2^(13 - HEAD) at b = 64, so
 //    Y = acc 2^-21 <= n_in 2^8 stays below fp16's max for n_in <= 255.
 //
-// LDS (138,816 B): two regions x 16 token slots of 4,160 B (a token's 32-block x chunk, 32 rows x
+// LDS (145,728 B): two regions x 16 token slots of 4,160 B (a token's 32-block x chunk, 32 rows x
 // 128 B -> X units (2 K-steps x 2 KiB, bcfft_dm64.hip's map) -> at the tile end Y half-units ->
-// y staging), the 4 KiB DFT table, the scales.
+// y staging), the 4 KiB DFT table (stage 3), stage 1's 8 KiB bf16 A fragments, the scales.
 #ifndef BCFFT_STREAM_POLICY
 #define BCFFT_STREAM_POLICY 3                       // write-through y stores (level to 1 % faster; nt x loads slower, profiles/r04_ab_stream_policy_split.log)
 #endif
@@ -32,7 +34,8 @@
 #include "bcfft_dm_table.h"
 #include "bcfft_dm_common.h"
 
-// stage 1 loads both quarters of a token's chunk before their two wave reductions, which then
+// the even / odd stage 1 (BCFFT_DM64K_F16S1) loads both quarters of a token's chunk before their
+// two wave reductions, which then
 // interleave (bit-identical; 2-3 % faster at N = 1024 and 8192, tools/ab_dm64k.py);
 // -DBCFFT_DM64K_NO_ILP builds the quarter-by-quarter order for A/B
 #ifndef BCFFT_DM64K_NO_ILP
@@ -51,7 +54,8 @@ constexpr int F_OFF = 2 * REGION;                   // DFT table image, 32 rows 
 constexpr int SC_OFF = F_OFF + 4096;                // scale exponents [16 tokens][2 quarters]
 constexpr int RR_OFF = SC_OFF + 128;                // per-token reference exponents [16]
 constexpr int OS_OFF = RR_OFF + 64;                 // the group's 32 inverse weight scales
-constexpr int LDS_BYTES = OS_OFF + 128;
+constexpr int TB_OFF = OS_OFF + 128;                // stage 1's bf16 hi + lo A fragments (kDmB64)
+constexpr int LDS_BYTES = TB_OFF + 8192;
 constexpr int FRAGS = BW * KC * NT;                 // B fragments per wave and chunk
 constexpr int NDMA = 2 * 4;                         // 1-KiB x DMA pieces per wave and chunk (2 tokens)
 constexpr int HEAD = 4;
@@ -70,6 +74,18 @@ __device__ __forceinline__ int yhalf64(int w, int o, int par) { return 2048 * pa
 // fp16 factor 2^-d (d >= -15) as a (lo, hi) pair: subnormal below 2^-14, zero below 2^-24
 __device__ __forceinline__ uint32_t f16_pow2_neg(int d) {
   return d <= 14 ? (uint32_t)(15 - d) << 10 : (d <= 24 ? 1u << (24 - d) : 0u);
+}
+// fp16 pair (a s, b s), each rounded once (v_fma_mix: f32 operands, f16 result in a half)
+__device__ __forceinline__ uint32_t pk_scaled(float a, float b, float s) {
+  uint32_t r;
+  asm("v_fma_mixlo_f16 %0, %1, %3, 0\n\tv_fma_mixhi_f16 %0, %2, %3, 0" : "=&v"(r) : "v"(a), "v"(b), "v"(s));
+  return r;
+}
+// per-half max of the bf16 magnitudes of two packed pairs (v_pk_max_u16 on the sign-cleared bits)
+typedef __attribute__((ext_vector_type(2))) unsigned short u16x2;
+__device__ __forceinline__ uint32_t pk_umax(uint32_t m, uint32_t w) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, m),
+                                                                __builtin_bit_cast(u16x2, w & 0x7fff7fffu)));
 }
 }  // namespace dm64k
 
@@ -96,16 +112,22 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
   const int64_t n_mtiles = (n_tokens + TT - 1) / TT;
   const int gstride = gm.stride;
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+#ifdef BCFFT_STAMPS
+  ANALYSIS_INIT;
+  (void)ablate_flags_;
+#endif
 
-  // ---- chunk c of tokens w and w + 8 of M-tile m -> their slots by LDS-DMA: piece q = rows
-  // 8q + (lane >> 3) of 128 B, unit u of row r at u ^ (r & 7); the buffer range ends at the row
-  // end, so a partial last chunk and tokens / tiles past the end land as zeros
-  auto dma_chunk = [&](int64_t m, int c, char* region) {
-    if constexpr ((ABL & 16) != 0) {                // keep the VMEM count: 8 empty-range loads
+  // ---- chunk c of token w + 8 t2 of M-tile m -> its slot by LDS-DMA: piece q = rows 8q +
+  // (lane >> 3) of 128 B, unit u of row r at u ^ (r & 7); the buffer range ends at the row end, so
+  // a partial last chunk and tokens / tiles past the end land as zeros. Issued inside stage 1
+  // (which has no other VMEM), so that its issue cost overlaps the stage's MFMAs
+  auto dma_tok = [&](int64_t m, int c, char* region, int t2) {
+    const int tl = wave + 8 * t2;
+    if constexpr ((ABL & 16) != 0) {                // keep the VMEM count: 4 empty-range loads
       const __amdgpu_buffer_rsrc_t zr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(xv), 0, 0, 0x00020000);
-      const uint32_t d0 = lds_base + (uint32_t)(region - lds) + wave * XSLOT;
+      const uint32_t d0 = lds_base + (uint32_t)(region - lds) + tl * XSLOT;
 #pragma unroll
-      for (int q = 0; q < NDMA; ++q) {
+      for (int q = 0; q < 4; ++q) {
         uint32_t keep;
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen" BCFFT_XPOL " lds\n\ts_mov_b32 m0, %0"
                      : "=&s"(keep) : "v"(0), "s"(zr), "s"(d0) : "memory");
@@ -115,21 +137,17 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
     const int dl = opaque(lane);
     const int r = dl >> 3;
     const int vb = r * 128 + 16 * ((dl & 7) ^ r);
+    const int64_t tok = m * TT + tl;
+    const bool ok = m < n_mtiles && tok < n_tokens;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>((const char*)xv) + (ok ? tok * KX * ES + (int64_t)c * 4096 : 0), 0,
+        ok ? (int)(KX * ES - (int64_t)c * 4096) : 0, 0x00020000);
+    const uint32_t dst0 = lds_base + (uint32_t)(region - lds) + tl * XSLOT;
 #pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2) {
-      const int tl = wave + 8 * t2;
-      const int64_t tok = m * TT + tl;
-      const bool ok = m < n_mtiles && tok < n_tokens;
-      const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<char*>((const char*)xv) + (ok ? tok * KX * ES + (int64_t)c * 4096 : 0), 0,
-          ok ? (int)(KX * ES - (int64_t)c * 4096) : 0, 0x00020000);
-      const uint32_t dst0 = lds_base + (uint32_t)(region - lds) + tl * XSLOT;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        uint32_t keep;
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen" BCFFT_XPOL " lds\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(vb), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
-      }
+    for (int q = 0; q < 4; ++q) {
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen" BCFFT_XPOL " lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(vb), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
     }
   };
 
@@ -140,9 +158,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
   const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint32_t*>(stat + 4) + ((int64_t)(grp_o * NW + wave) * npiece) * 256, 0, npiece * 1024, 0x00020000);
   // fragment (fb, j, nt) of chunk c; K-step 2c + 1 past the image (odd KS, last chunk) reads zeros
-  auto load_b1 = [&](int c, int fb, int j, int nt, u32x4 (&breg)[BW][KC][NT]) {
+  auto load_b1 = [&](int c, int fb, int j, int nt, u32x4 (&breg)[BW][KC][NT], bool live) {
     const int ks = 2 * c + j;
-    const int vo = opaque(lane) * 16 + (ks < KS && (ABL & 1) == 0 ? (fb * KS + ks) * 2 + nt : npiece) * 1024;
+    const int vo = opaque(lane) * 16 + (live && ks < KS && (ABL & 1) == 0 ? (fb * KS + ks) * 2 + nt : npiece) * 1024;
     asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(breg[fb][j][nt]) : "v"(vo), "s"(brs));
   };
   auto wait_b = [&](auto n_tag, u32x4 (&breg)[BW][KC][NT]) {
@@ -158,21 +176,108 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
   static_assert(FRAGS == 16, "wait_b names sixteen fragments");
 
   // ---- prologue: the first tile's chunk 0, the DFT table, the inverse weight scales
-  dma_chunk(wg_in_grp, 0, lds);
+  dma_tok(wg_in_grp, 0, lds, 0);
+  dma_tok(wg_in_grp, 0, lds, 1);
   if (tid < 256) {                                  // chunk c: row c >> 3, chunk c & 7
     const uint4* tab = reinterpret_cast<const uint4*>(kDmF64);
     const int t = tid >> 3, ch = tid & 7;
     *reinterpret_cast<uint4*>(lds + F_OFF + 128 * t + 16 * (ch ^ fsw64(t))) = tab[tid];
   }
   if (tid < 32) reinterpret_cast<float*>(lds + OS_OFF)[tid] = osc[grp_o * 32 + tid];
+  reinterpret_cast<uint4*>(lds + TB_OFF)[tid] = reinterpret_cast<const uint4*>(kDmB64)[tid];
   wait_vmcnt<0>();
   lds_barrier();
 
-  // ---- stage 1 (wave w: tokens w, w + 8): bcfft_dm64.hip's stage 1 on the chunk's two quarters,
-  // the scale of each lowered by HEAD bits
-  auto stage1 = [&](char* region) {
+  // ---- stage 1 (wave w: tokens w, w + 8) on the raw bf16 x of the chunk's two quarters: the
+  // 64-point transform F x as bf16 MFMAs, F 2^-7 as hi + lo A fragments (kDmB64, ~16 significant
+  // bits; x_{t+32} enters the odd-bin tiles negated, F_{t+32} = -F_t there), fp32 accumulation,
+  // then X 2^sx rounded once to fp16. sx is the per-(token, quarter) scale of the even / odd
+  // form below (max |x| from the bf16 magnitude bits, HEAD bits lower), so X keeps its bound and
+  // stage 2 is unchanged. Per quarter and lane: 17 VALU for the max and 16 for scale + rounding
+  // against ~100 for unpack / scale / a, d / rounding; 16 MFMAs instead of 4, issued as soon as
+  // x is read (the max reduction runs under them). Products of x below ~2^-110 fall into fp32's
+  // subnormal range, as in the reference's fp32 rfft.
+#ifndef BCFFT_DM64K_F16S1
+  auto stage1 = [&](char* region, auto&& dma) {
     if constexpr ((ABL & 2) != 0) {
       if (lane < 2) { wsc[wave * 2 + lane] = 0; wsc[(wave + 8) * 2 + lane] = 0; }
+      dma(0);
+      dma(1);
+      return;
+    }
+    const int l = opaque(lane);
+    const int b16 = l & 15, g = l >> 4;
+    int xwb[2];
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) xwb[pr] = 256 * g + 64 * (pr ^ (g & 1)) + 4 * b16;
+#pragma unroll 1
+    for (int t2 = 0; t2 < 2; ++t2) {
+      const int tl = wave + 8 * t2;
+      char* slot = region + tl * XSLOT;
+      uint4 xr[KC][2];
+#pragma unroll
+      for (int h = 0; h < KC; ++h)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt)
+          xr[h][pt] = *reinterpret_cast<const uint4*>(slot + (16 * h + b16) * (B * ES) + 16 * ((g + 4 * pt) ^ (b16 & 7)));
+      dma(t2);                                      // the next step's x of this token slot
+      f32x4 acc4[KC][4];
+#pragma unroll
+      for (int h = 0; h < KC; ++h) {
+        const uint4 xn = make_uint4(xr[h][1].x ^ 0x80008000u, xr[h][1].y ^ 0x80008000u, xr[h][1].z ^ 0x80008000u,
+                                    xr[h][1].w ^ 0x80008000u);
+        const bf16x8 b0 = __builtin_bit_cast(bf16x8, xr[h][0]), b1 = __builtin_bit_cast(bf16x8, xr[h][1]);
+        const bf16x8 b1n = __builtin_bit_cast(bf16x8, xn);
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) {
+            const char* tb = lds + TB_OFF + 2048 * (2 * pr + mt) + 16 * l;
+            const bf16x8 th = *reinterpret_cast<const bf16x8*>(tb), tlo = *reinterpret_cast<const bf16x8*>(tb + 1024);
+            f32x4 a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(th, b0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tlo, b0, a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(th, pr ? b1n : b1, a, 0, 0, 0);
+            acc4[h][2 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tlo, pr ? b1n : b1, a, 0, 0, 0);
+          }
+      }
+      uint32_t mq[KC];
+#pragma unroll
+      for (int h = 0; h < KC; ++h) {
+        uint32_t m0 = pk_umax(0u, xr[h][0].x), m1 = pk_umax(0u, xr[h][0].y);
+        m0 = pk_umax(m0, xr[h][0].z); m1 = pk_umax(m1, xr[h][0].w);
+        m0 = pk_umax(m0, xr[h][1].x); m1 = pk_umax(m1, xr[h][1].y);
+        m0 = pk_umax(m0, xr[h][1].z); m1 = pk_umax(m1, xr[h][1].w);
+        const uint32_t m = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, m0),
+                                                                                  __builtin_bit_cast(u16x2, m1)));
+        mq[h] = max(m & 0xffffu, m >> 16) << 16;    // fp32 bits of the lane's max |x|
+      }
+#pragma unroll
+      for (int h = 0; h < KC; ++h) mq[h] = wave_umax(mq[h]);
+#pragma unroll
+      for (int h = 0; h < KC; ++h) {
+        const int sx = stat_scale_exp(2.f * __uint_as_float(mq[h])) - HEAD;
+        if (l == 0) wsc[tl * 2 + h] = sx - 7;      // X = D 2^-(sx - 7): the table's 2^-7
+        const float S = __int_as_float((sx + 127) << 23);
+        char* xb = slot + 2048 * h;
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) {
+            const f32x4 v = acc4[h][2 * pr + mt];
+            *reinterpret_cast<uint32_t*>(xb + xwb[pr] + 1024 * mt) = pk_scaled(v[0], v[1], S);
+            *reinterpret_cast<uint32_t*>(xb + xwb[pr] + 1024 * mt + 128) = pk_scaled(v[2], v[3], S);
+          }
+      }
+    }
+  };
+#else
+  // the even / odd form (bcfft_dm64.hip's stage 1: a = x_t + x_{t+32}, d = x_t - x_{t+32} scaled
+  // and rounded to fp16, F 2^-7 as one fp16 term), kept for A/B
+  auto stage1 = [&](char* region, auto&& dma) {
+    if constexpr ((ABL & 2) != 0) {
+      if (lane < 2) { wsc[wave * 2 + lane] = 0; wsc[(wave + 8) * 2 + lane] = 0; }
+      dma(0);
+      dma(1);
       return;
     }
     const int l = opaque(lane);
@@ -188,6 +293,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
     for (int t2 = 0; t2 < 2; ++t2) {
       const int tl = wave + 8 * t2;
       char* slot = region + tl * XSLOT;
+      dma(t2);
 #ifdef BCFFT_DM64K_ILP
       // both quarters' x and maxima first, so their two wave reductions (DPP + readlane chains)
       // can interleave; the per-quarter scales, and so every result, are unchanged
@@ -293,6 +399,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
       }
     }
   };
+#endif
 
   // accumulators [bin of the wave][M-tile][N-tile]: rows 4 yt + r = token 8 mt + 2 yt + (r >> 1),
   // re / im r & 1; reference exponents of the A-row tokens and the accumulator-row tokens
@@ -370,28 +477,42 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
       }
     const int sw = 64 * (wave & 1);
     // B of this step: younger VMEM is this step's x DMA and, at a tile's first chunk, the
-    // previous tile's stage-3 stores before it
-    if (tile0) wait_b(std::integral_constant<int, 8 + NDMA>{}, breg);
-    else wait_b(std::integral_constant<int, NDMA>{}, breg);
-    const int nc = nb < 0 ? 0 : nb;
+    // previous tile's stage-3 stores before it. One operand-carrying wait on every path (a wait
+    // per branch made the compiler copy the 16 fragments where the paths join)
+    if (!tile0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");
+    wait_b(std::integral_constant<int, 8 + NDMA>{}, breg);
+    const bool more = nb >= 0;
+    const int nc = more ? nb : 0;
+    // A rows of bin 4 wave + fb: X units of the 8 tokens of M-tile mt, K-step j; the next bin's
+    // four units are read while this bin's are scaled and multiplied (LDS latency off the chain)
+    const char* abase = region + a_t * XSLOT + 256 * wave + 16 * kb;
+    auto a_off = [&](int fb, int j, int mt) { return 8 * mt * XSLOT + ((fb & 1) ? -sw : sw) + 64 * fb + 2048 * j; };
+    uint4 araw[2][KC][MT];
+#pragma unroll
+    for (int j = 0; j < KC; ++j)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) araw[0][j][mt] = *reinterpret_cast<const uint4*>(abase + a_off(0, j, mt));
+    const bool bin0 = wave == 0;                    // bin 0 (wave 0, fb 0): (X_0, X_32), no swap
 #pragma unroll
     for (int fb = 0; fb < BW; ++fb) {
-      const int f = wave * BW + fb;
+      if (fb + 1 < BW) {
+#pragma unroll
+        for (int j = 0; j < KC; ++j)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+            araw[(fb + 1) & 1][j][mt] = *reinterpret_cast<const uint4*>(abase + a_off(fb + 1, j, mt));
+      }
+      const uint32_t sel = (fb == 0 && bin0) ? 0x03020100u : a_sel;
 #pragma unroll
       for (int j = 0; j < KC; ++j) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-          const char* ab = region + (8 * mt + a_t) * XSLOT + 256 * wave + 16 * kb + ((fb & 1) ? -sw : sw) + 64 * fb + 2048 * j;
-          uint4 raw = *reinterpret_cast<const uint4*>(ab);
-          if (f == 0) {
-            raw.x = pkmul(raw.x, amul0[mt][j]); raw.y = pkmul(raw.y, amul0[mt][j]);
-            raw.z = pkmul(raw.z, amul0[mt][j]); raw.w = pkmul(raw.w, amul0[mt][j]);
-          } else {
-            raw.x = pkmul(__builtin_amdgcn_perm(raw.x, raw.x, a_sel), amul[mt][j]);
-            raw.y = pkmul(__builtin_amdgcn_perm(raw.y, raw.y, a_sel), amul[mt][j]);
-            raw.z = pkmul(__builtin_amdgcn_perm(raw.z, raw.z, a_sel), amul[mt][j]);
-            raw.w = pkmul(__builtin_amdgcn_perm(raw.w, raw.w, a_sel), amul[mt][j]);
-          }
+          const uint32_t mul = (fb == 0 && bin0) ? amul0[mt][j] : amul[mt][j];
+          uint4 raw = araw[fb & 1][j][mt];
+          raw.x = pkmul(__builtin_amdgcn_perm(raw.x, raw.x, sel), mul);
+          raw.y = pkmul(__builtin_amdgcn_perm(raw.y, raw.y, sel), mul);
+          raw.z = pkmul(__builtin_amdgcn_perm(raw.z, raw.z, sel), mul);
+          raw.w = pkmul(__builtin_amdgcn_perm(raw.w, raw.w, sel), mul);
           const f16x8 a = __builtin_bit_cast(f16x8, raw);
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt)
@@ -401,10 +522,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
               acc[fb][mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, __builtin_bit_cast(f16x8, breg[fb][j][nt]),
                                                                        acc[fb][mt][nt], 0, 0, 0);
         }
-        if (nb >= 0) {
-          load_b1(nc, fb, j, 0, breg);
-          load_b1(nc, fb, j, 1, breg);
-        }
+        // the next step's fragments; past the last step an empty-range load (no branch, no copy)
+        load_b1(nc, fb, j, 0, breg, more);
+        load_b1(nc, fb, j, 1, breg, more);
       }
     }
   };
@@ -544,48 +664,60 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
   // region holding chunk c's x; the other holds the previous chunk's X or, at c = 0, the
   // previous tile's Y units):
   //   c = 0   stage 3 of the previous tile's tokens w, w + 8 from the other region (8 stores)
-  //           x DMA of the next step's chunk into the other region (zeros past the last tile);
-  //           x(m, c) landed; stage 1                                                        | Ba |
+  //           x(m, c) landed; stage 1, per token slot issuing the x DMA of the next step's
+  //           chunk into the other region (zeros past the last tile)                         | Ba |
   //           stage 2 on B(c) (loaded in the previous step), loading the next step's B      | Bb |
   //   c last  Y of the tile into this region                                                 | Be |
-  // VMEM younger than x(m, c) when it is waited for: B(c) 16 (the previous step's stage 2), at
-  // c = 0 the 8 stores, then the DMA (the first step's x and B were waited for up front).
+  // VMEM younger than x(m, c) when it is waited for: B(c) 16 (the previous step's stage 2) and,
+  // at c = 0, the 8 stores (the first step's x and B were waited for up front).
   u32x4 breg[BW][KC][NT];
 #pragma unroll
   for (int fb = 0; fb < BW; ++fb)
 #pragma unroll
     for (int j = 0; j < KC; ++j) {
-      load_b1(0, fb, j, 0, breg);
-      load_b1(0, fb, j, 1, breg);
+      load_b1(0, fb, j, 0, breg, true);
+      load_b1(0, fb, j, 1, breg, true);
     }
   wait_vmcnt<0>();
   int rsel = 0;
   int64_t mprev = -1;
   int64_t m = wg_in_grp;
   int c = 0;
+  // stamps build: slots 8 c + phase for the steps of the workgroup's second tile
+  [[maybe_unused]] int tcount = 0;
+#define DST(o) do { if (tcount == 1 && c < 7) STAMP(8 * c + (o)); } while (0)
   while (m < n_mtiles) {
     char* region = lds + rsel * REGION;
     char* other = lds + (rsel ^ 1) * REGION;
     const bool tile0 = c == 0;
+    DST(0);
     if (tile0) {
       stage3(other, wave, wrr[wave], mprev >= 0 ? mprev * TT + wave : -1);
       stage3(other, wave + 8, wrr[wave + 8], mprev >= 0 ? mprev * TT + wave + 8 : -1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slots' staging reads are done
     }
+    DST(1);
     const bool last = c + 1 == nch;
     const int64_t mn = last ? m + gstride : m;
     const int cn = last ? 0 : c + 1;
-    dma_chunk(mn, cn, other);
-    if (tile0) wait_vmcnt<FRAGS + 8 + NDMA>();
-    else wait_vmcnt<FRAGS + NDMA>();
-    stage1(region);
+    DST(2);
+    // x(m, c) landed: younger VMEM is B(c) (the previous step's stage 2) and, at c = 0, the stores
+    if (tile0) wait_vmcnt<FRAGS + 8>();
+    else wait_vmcnt<FRAGS>();
+    DST(3);
+    stage1(region, [&](int t2) { dma_tok(mn, cn, other, t2); });
+    DST(4);
     lds_barrier();                                  // Ba: X units and quarter scales complete
+    DST(5);
     stage2(region, breg, mn < n_mtiles ? cn : -1, tile0, tile0);
+    DST(6);
     lds_barrier();                                  // Bb: every read of this chunk's X done
+    DST(7);
     if (last) {
       ywrite(region);
       lds_barrier();                                // Be: Y units and reference exponents
       mprev = m;
+      ++tcount;
     }
     rsel ^= 1;
     m = mn;
@@ -594,7 +726,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
   char* yreg = lds + (rsel ^ 1) * REGION;
   stage3(yreg, wave, wrr[wave], mprev >= 0 ? mprev * TT + wave : -1);
   stage3(yreg, wave + 8, wrr[wave + 8], mprev >= 0 ? mprev * TT + wave + 8 : -1);
+  wait_vmcnt<0>();                                  // the last step's empty-range B loads
 }
+
+#undef DST
 
 bool dm64k_eligible(int n_in, int b, int xdt, bool yf32) {
   return dm64k_geometry(n_in, b) && xdt == BCFFT_BF16 && !yf32;
@@ -613,3 +748,10 @@ void launch_forward_dm64k(const void* x, int64_t n, int n_in, int n_out, const v
 }
 
 }  // namespace bcfft
+
+#ifdef BCFFT_STAMPS
+extern "C" int bcfft_set_stamps_dm64k(void* buf) {
+  unsigned long long* p = (unsigned long long*)buf;
+  return hipMemcpyToSymbol(HIP_SYMBOL(bcfft::g_stamps), &p, sizeof(p)) == hipSuccess ? 0 : BCFFT_ERR_HIP;
+}
+#endif

@@ -6,7 +6,9 @@ of its half: (re, im) of X_f, and for f = 0 (X_0, X_64).
   Fe[t][2j]   = cos(2 pi j t / 64),  Fe[t][2j+1] = -sin(2 pi j t / 64)   (j >= 1)
   Fe[t][0]    = 1,                   Fe[t][1]    = (-1)^t                 (X_0, X_64)
   Fo[t][2j]   = cos(2 pi (2j+1) t / 128), Fo[t][2j+1] = -sin(2 pi (2j+1) t / 128)
-Also kDmF64, the b = 64 table of bc_forward_dm64_kernel (bcfft_dm64.hip), built the same way.
+Also kDmF64, the b = 64 table of bc_forward_dm64_kernel (bcfft_dm64.hip), built the same way,
+and kDmB64, the same b = 64 table as bf16 hi + lo MFMA A fragments (bc_forward_dm64k_kernel's
+stage 1 on raw bf16 x).
 The precise engine (BCFFT_ALGO_DFTP, bcfft_dm.hip's EP variant) takes the same table times 2^8 as
 fp16 (kDmFp: entries 12.6 .. 256, the same 11 significant bits) plus its rounding residual
 F 2^8 - kDmFp as OCP e4m3 (kDmFl8, |value| <= 2^-3), pair-packed for the kernel's fp8 MFMA
@@ -48,6 +50,36 @@ for j in range(16):
     F64[:, 32 + 2 * j + 1] = -np.sin(th)
 bits64 = (F64 * 2.0 ** -7).astype(np.float16).view(np.uint16).astype(np.uint32)
 words64 = (bits64[:, 0::2] | (bits64[:, 1::2] << 16)).reshape(-1)     # (32 rows x 32 words)
+
+
+def bf16_rne(v):
+    """v rounded to bf16 (8 significant bits, round half to even) in fp64; normal range only."""
+    m, e = np.frexp(np.asarray(v, np.float64))
+    return np.ldexp(np.round(m * 256.0), e - 8)
+
+
+def bf16_bits(v):
+    """bf16 bits of values exactly representable in bf16."""
+    return (np.asarray(v, np.float32).view(np.uint32) >> 16).astype(np.uint32)
+
+
+# b = 64, the bf16 direct stage 1 of bc_forward_dm64k_kernel (bcfft_dm64k.hip): the MFMA A
+# fragments of F64 2^-7 as bf16 hi + lo (hi = bf16(v), lo = bf16(v - hi): ~16 significant bits).
+# Fragment (pr, mt, term), lane l, element e = A[m = l & 15][k = 8 (l >> 4) + e] = column
+# 32 pr + 16 mt + m, row t = k; layout [pr][mt][term][lane][8 bf16] (16 B per lane)
+v64 = F64 * 2.0 ** -7
+hi64 = bf16_rne(v64)
+lo64 = bf16_rne(v64 - hi64)
+assert np.abs(v64 - hi64 - lo64).max() <= 2.0 ** -23
+fragb = np.zeros((2, 2, 2, 64, 8), np.uint32)
+for pr in range(2):
+    for mt in range(2):
+        for ln in range(64):
+            col = 32 * pr + 16 * mt + (ln & 15)
+            ts = 8 * (ln >> 4) + np.arange(8)
+            fragb[pr, mt, 0, ln] = bf16_bits(hi64[ts, col])
+            fragb[pr, mt, 1, ln] = bf16_bits(lo64[ts, col])
+wordsb64 = (fragb[..., 0::2] | (fragb[..., 1::2] << 16)).reshape(-1)  # 2048 words
 
 
 def e4m3(v):
@@ -92,6 +124,11 @@ with open(out, "w") as f:
     f.write("__device__ const uint32_t kDmF64[1024] __attribute__((aligned(16))) = {\n")
     for r in range(0, 1024, 8):
         f.write("  " + ", ".join("0x%08xu" % w for w in words64[r:r + 8]) + ",\n")
+    f.write("};\n")
+    f.write("// F64 * 2^-7 as bf16 hi + lo MFMA A fragments [pr][mt][term][lane][8] (bcfft_dm64k.hip)\n")
+    f.write("__device__ const uint32_t kDmB64[2048] __attribute__((aligned(16))) = {\n")
+    for r in range(0, 2048, 8):
+        f.write("  " + ", ".join("0x%08xu" % w for w in wordsb64[r:r + 8]) + ",\n")
     f.write("};\n")
     f.write("// F[t][col] * 2^8 as fp16 pairs (the precise engine), layout of kDmF\n")
     f.write("__device__ const uint32_t kDmFp[4096] __attribute__((aligned(16))) = {\n")
