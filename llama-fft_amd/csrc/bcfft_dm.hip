@@ -909,7 +909,8 @@ bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, int mode, const void
   // the per-element path of BM = -1 costs ~50 % at the north star's size
   const int bm = bias_dt == BCFFT_NONE ? 0 : bias_dt == BCFFT_F32 ? 1 : 2;
 #define BCFFT_DM_LAUNCH_EX(XT, EXV)                                                                       \
-  (!yf32 || bm == 0 ? launch_dm<XT, true, EXV>(x, n, n_out, spec, bias, bias_dt, y, s)                  \
+  (!yf32            ? launch_dm<XT, true, EXV>(x, n, n_out, spec, bias, bias_dt, y, s)                  \
+   : bm == 0        ? launch_dm<XT, true, EXV, false, 0, 0>(x, n, n_out, spec, bias, bias_dt, y, s)     \
    : bm == 1        ? launch_dm<XT, true, EXV, false, 0, 1>(x, n, n_out, spec, bias, bias_dt, y, s)     \
                     : launch_dm<XT, true, EXV, false, 0, 2>(x, n, n_out, spec, bias, bias_dt, y, s))
 #define BCFFT_DM_LAUNCH(XT, YF)                                                                           \

@@ -52,13 +52,15 @@ def main():
     xd = torch.from_numpy(x).to(dev)
     with torch.inference_mode():
         y = sharded_forward(layer, xd)                   # shard + RCCL all_gather_into_tensor
-        y2 = gather_rows(layer(xd[:500]), 500)          # a second gather of another size
+        # a second gather of another size; 600 tokens keep AUTO on the engine of the 1003-token
+        # call (up to 512 it takes the short-N kernel, whose roundings differ)
+        y2 = gather_rows(layer(xd[:600]), 600)
     torch.cuda.synchronize()
     ref = O.bc_forward(x, c, bv)
     g = y.cpu().numpy()
     err = float(np.linalg.norm(g - ref) / np.linalg.norm(ref))
     assert y.shape == (n, k) and err < 6e-4, err
-    assert torch.equal(y2, y[:500])
+    assert torch.equal(y2, y[:600])
 
     r = bench.run_partitioned(layer, xd, n, 3, 1, 1, barrier, dev, settle_ms=0.0, allgather=True, repeats=2)
     assert r["gather_wall"] is not None and r["gather_wall"] > 0 and r["wall"] > 0, r

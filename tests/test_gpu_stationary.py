@@ -44,6 +44,25 @@ def _run(dev, x, c, bv, xdt, mdt, algo="stationary"):
     return y, ref
 
 
+def _auto_is_short(n, k, m, b, xdt, ydt=None):
+    """True where AUTO takes the short-N kernel (bc_forward_sn_kernel) for these sizes: its grid
+    fits one round of CUs on the STAT geometries; the persistent engine named by a test is then
+    not AUTO's choice, so AUTO is checked against the oracle instead of bit-equality."""
+    from bcfft import _lib
+    lib = _lib.load()
+    cx = _lib.dtype_code(TDT[xdt])
+    cy = _lib.dtype_code(TDT[ydt or xdt])
+    return lib.bcfft_forward_resolve(n, k, m, b, 0, cx, cy) == _lib.ALGOS["short"]
+
+
+def _check_auto(y, ya, ref, n, k, m, b, xdt, ydt=None):
+    """AUTO's output: bit-equal to the named engine's y, or (short-N) within the same bounds."""
+    if _auto_is_short(n, k, m, b, xdt, ydt):
+        _check(ya, ref, xdt)
+    else:
+        assert torch.equal(y, ya)
+
+
 def _check(y, ref, xdt="float32"):
     g = y.detach().float().cpu().numpy()
     assert g.shape == ref.shape
@@ -94,7 +113,7 @@ def test_auto_resolution_for_eligible_shapes(dev):
     DFT kernel for bf16 I/O: same bits as the explicit algorithm."""
     rng = np.random.default_rng(1)
     c = (rng.standard_normal((32, 32, 128)) * 0.01).astype(np.float32)
-    x = rng.standard_normal((12, 4096)).astype(np.float32)
+    x = rng.standard_normal((1100, 4096)).astype(np.float32)   # above the short-N crossover
     ya, _ = _run(dev, x, c, None, "float32", "float32", algo="auto")
     yd, _ = _run(dev, x, c, None, "float32", "float32", algo="dftx")
     assert torch.equal(ya, yd)
