@@ -544,7 +544,10 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
   // ntm: the N-tiles this wave does (3: both, the I wave of a steady-state tile; the last pass
   // splits them between the slot's F and I waves, which then meet at a barrier between their Y
   // reads and staging writes: the staging of one N-tile overlays the Y units of both)
-  auto stage3 = [&](char* region, int par, int64_t mp, int ntm) {
+  // (a compile-time mask: a runtime one split the stage into ~30 basic blocks, one per N-tile's
+  // MFMAs and staging writes, which the scheduler could not interleave)
+  auto stage3 = [&](char* region, int par, int64_t mp, auto ntm_c) {
+    constexpr int ntm = decltype(ntm_c)::value;
     const int l = opaque(lane);
     const int o16 = l & 15, g = l >> 4;
     char* slot = region + tslot * SLOT;
@@ -586,7 +589,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
     f16x8 gcur[KS][2], gnxt[KS][2];
     gload(0, gcur);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // Y is in registers: the slot is free
-    if (ntm != 3) lds_barrier();                    // ... for both waves of the slot
+    if constexpr (ntm != 3) lds_barrier();          // ... for both waves of the slot
     SUBSTAMP(55);
     SUBSTAMP(56);
     const int64_t tok = mp * TT + tslot;
@@ -816,10 +819,11 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
         else if (!XW) wait_vmcnt<0>();              // this wave's own x DMA (issued a phase ahead)
         stage1(region, par, 3, XW && it > 0);
       } else if (DRAIN_SPLIT) {                     // drain: the last tile's stage 3, N-tile 1
-        stage3(other, par ^ 1, m - gstride, 2);
+        stage3(other, par ^ 1, m - gstride, std::integral_constant<int, 2>{});
       }
     } else if (it > 0) {
-      stage3(other, par ^ 1, m - gstride, DRAIN_SPLIT && !have_f ? 1 : 3);
+      if (DRAIN_SPLIT && !have_f) stage3(other, par ^ 1, m - gstride, std::integral_constant<int, 1>{});
+      else stage3(other, par ^ 1, m - gstride, std::integral_constant<int, 3>{});
     }
     if constexpr (LATE_W) creg_tie();               // the weights, first needed by stage 2
     STAMP(sb + 1);
