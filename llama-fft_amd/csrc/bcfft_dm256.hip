@@ -63,6 +63,9 @@ __device__ __forceinline__ int xunit(int k, int q) { return 64 * k + 16 * q; }
 __device__ __forceinline__ int yunit(int s, int w, int o, int par) { return 1024 * w + 512 * s + 256 * par + 16 * o; }
 }  // namespace d256
 
+// HB: a bias is added (the runtime bias_dt then names its dtype); without one the store path is
+// straight-line (a runtime test per stored quad split stage 3 into hundreds of basic blocks)
+template <bool HB>
 __global__ __launch_bounds__(512, 2) void bc_forward_dm256_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_out, const uint32_t* __restrict__ stat,
     const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
@@ -412,7 +415,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256_kernel(
           lo[r] = (e + o) * ysc;                    // y_t
           hi[r] = (e - o) * ysc;                    // y_{t+128}
         }
-        if (bias_dt != BCFFT_NONE) {                // .to(x dtype) :266, + bias :270-271
+        if (HB) {                                   // .to(x dtype) :266, + bias :270-271
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             lo[r] = round_to(lo[r], XT);
@@ -511,6 +514,7 @@ __device__ __forceinline__ uint32_t f16_pow2_neg(int d) {
 }
 }  // namespace d256
 
+template <bool HB>
 __global__ __launch_bounds__(512, 2) void bc_forward_dm256k_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_in, int n_out, const uint32_t* __restrict__ stat,
     const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
@@ -909,7 +913,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256k_kernel(
           lo[r] = (e + o) * ysc;
           hi[r] = (e - o) * ysc;
         }
-        if (bias_dt != BCFFT_NONE) {                // .to(x dtype) :266, + bias :270-271
+        if (HB) {                                   // .to(x dtype) :266, + bias :270-271
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             lo[r] = round_to(lo[r], XT);
@@ -1011,7 +1015,7 @@ constexpr int LDSG_BYTES = OSG_OFF + MAXG * NOB * 4;
 static_assert(LDSG_BYTES <= 160 * 1024, "LDS budget");
 }  // namespace d256
 
-template <bool GLU>
+template <bool GLU, bool HB>
 __global__ __launch_bounds__(512, 2) void bc_forward_dm256g_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_out, const uint32_t* __restrict__ stat,
     const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
@@ -1390,7 +1394,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256g_kernel(
             lo[r] = round_to(round_to(silu(lo[r]), XT) * ulo, XT);
             hi[r] = round_to(round_to(silu(hi[r]), XT) * uhi, XT);
           }
-        } else if (bias_dt != BCFFT_NONE) {         // .to(x dtype) :266, + bias :270-271
+        } else if (HB) {                            // .to(x dtype) :266, + bias :270-271
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             lo[r] = round_to(lo[r], XT);
@@ -1495,16 +1499,27 @@ void launch_forward_dm256(const void* x, int64_t n, int n_in, int n_out, const v
   const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
   if (dm256g_taken(n, n_in, n_out)) {             // x transformed once
     const int64_t wgs = device_cu_count() < n_mtiles ? device_cu_count() : n_mtiles;
-    hipLaunchKernelGGL(bc_forward_dm256g_kernel<false>, dim3((unsigned)wgs), dim3(512), 0, s, x, n, n_out, stat, osc,
-                       bias, bias_dt, y);
+    if (bias_dt != BCFFT_NONE)
+      hipLaunchKernelGGL((bc_forward_dm256g_kernel<false, true>), dim3((unsigned)wgs), dim3(512), 0, s, x, n, n_out, stat,
+                         osc, bias, bias_dt, y);
+    else
+      hipLaunchKernelGGL((bc_forward_dm256g_kernel<false, false>), dim3((unsigned)wgs), dim3(512), 0, s, x, n, n_out, stat,
+                         osc, bias, bias_dt, y);
     return;
   }
-  if (n_in == d256::NI)
-    hipLaunchKernelGGL(bc_forward_dm256_kernel, dim3((unsigned)total), dim3(512), 0, s, x, n, n_out, stat, osc, bias,
-                       bias_dt, y);
-  else
-    hipLaunchKernelGGL(bc_forward_dm256k_kernel, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat, osc,
+  const bool hb = bias_dt != BCFFT_NONE;
+  if (n_in == d256::NI && hb)
+    hipLaunchKernelGGL(bc_forward_dm256_kernel<true>, dim3((unsigned)total), dim3(512), 0, s, x, n, n_out, stat, osc,
                        bias, bias_dt, y);
+  else if (n_in == d256::NI)
+    hipLaunchKernelGGL(bc_forward_dm256_kernel<false>, dim3((unsigned)total), dim3(512), 0, s, x, n, n_out, stat, osc,
+                       bias, bias_dt, y);
+  else if (hb)
+    hipLaunchKernelGGL(bc_forward_dm256k_kernel<true>, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat,
+                       osc, bias, bias_dt, y);
+  else
+    hipLaunchKernelGGL(bc_forward_dm256k_kernel<false>, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat,
+                       osc, bias, bias_dt, y);
 }
 }  // namespace bcfft
 
@@ -1524,7 +1539,7 @@ void launch_forward_dm256_glu(const void* x, int64_t n, int n_gate, const void* 
   const int64_t wgs = device_cu_count() < n_mtiles ? device_cu_count() : n_mtiles;
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
   const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
-  hipLaunchKernelGGL(bc_forward_dm256g_kernel<true>, dim3((unsigned)wgs), dim3(512), 0, s, x, n, n_gate, stat, osc,
+  hipLaunchKernelGGL((bc_forward_dm256g_kernel<true, false>), dim3((unsigned)wgs), dim3(512), 0, s, x, n, n_gate, stat, osc,
                      nullptr, BCFFT_NONE, h);
 }
 }  // namespace bcfft

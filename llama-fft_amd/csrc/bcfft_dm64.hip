@@ -45,7 +45,9 @@ __device__ __forceinline__ int xunit64(int ks, int f, int q) { return 2048 * ks 
 __device__ __forceinline__ int yhalf64(int w, int o, int par) { return 2048 * par + 256 * w + 8 * (o ^ (16 * ((w >> 1) & 1))); }
 }  // namespace dm64
 
-template <bool GLU>
+// HB: a bias is added (the runtime bias_dt then names its dtype); without one the store path is
+// straight-line (a runtime test per stored quad split stage 3 into hundreds of basic blocks)
+template <bool GLU, bool HB>
 __global__ __launch_bounds__(512, 2) void bc_forward_dm64_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_out, const uint32_t* __restrict__ stat,
     const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
@@ -341,7 +343,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64_kernel(
             float v[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = hf ? fmaf(E[nt][r], ysc[nt], -os[r]) : fmaf(E[nt][r], ysc[nt], os[r]);
-            if (bias_dt != BCFFT_NONE) {            // .to(x dtype) :266, + bias :270-271
+            if (HB) {                               // .to(x dtype) :266, + bias :270-271
 #pragma unroll
               for (int r = 0; r < 4; ++r) v[r] = round_to(v[r], XT);
               if (o < nvalid) {
@@ -406,7 +408,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64_kernel(
 }  // namespace bcfft
 
 namespace {
-template <bool GLU>
+template <bool GLU, bool HB>
 void launch_dm64(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt, void* y,
                  hipStream_t s) {
   const int groups = GLU ? (n_out + 15) / 16 : (n_out + 31) / 32;
@@ -415,7 +417,7 @@ void launch_dm64(const void* x, int64_t n, int n_out, const void* spec, const vo
   const int64_t total = bcfft::group_grid(bcfft::device_cu_count(), groups, n_mtiles);
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
   const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
-  hipLaunchKernelGGL((bcfft::bc_forward_dm64_kernel<GLU>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_out, stat,
+  hipLaunchKernelGGL((bcfft::bc_forward_dm64_kernel<GLU, HB>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_out, stat,
                      osc, bias, bias_dt, y);
 }
 }  // namespace
@@ -432,7 +434,8 @@ void launch_forward_dm64(const void* x, int64_t n, int n_out, const void* spec, 
     return;
   }
 #endif
-  if (glu) launch_dm64<true>(x, n, n_out, spec, nullptr, BCFFT_NONE, y, s);
-  else launch_dm64<false>(x, n, n_out, spec, bias, bias_dt, y, s);
+  if (glu) launch_dm64<true, false>(x, n, n_out, spec, nullptr, BCFFT_NONE, y, s);
+  else if (bias_dt != BCFFT_NONE) launch_dm64<false, true>(x, n, n_out, spec, bias, bias_dt, y, s);
+  else launch_dm64<false, false>(x, n, n_out, spec, bias, bias_dt, y, s);
 }
 }  // namespace bcfft

@@ -58,7 +58,9 @@ __host__ __device__ constexpr int pass_nt(int p) { return p >> 1; }
 __host__ __device__ constexpr int pass_ks(int p, int j) { return 2 * (p & 1) + (j & 1); }
 }  // namespace dm64g
 
-template <bool GLU>
+// HB: a bias is added (the runtime bias_dt then names its dtype); without one the store path is
+// straight-line (a runtime test per stored quad split stage 3 into hundreds of basic blocks)
+template <bool GLU, bool HB>
 __global__ __launch_bounds__(512, 2) void bc_forward_dm64g_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_out, const uint32_t* __restrict__ stat,
     const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
@@ -368,7 +370,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64g_kernel(
             float v[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = hf ? fmaf(E[nt][r], ysc[nt], -os[r]) : fmaf(E[nt][r], ysc[nt], os[r]);
-            if (bias_dt != BCFFT_NONE) {            // .to(x dtype) :266, + bias :270-271
+            if (HB) {                               // .to(x dtype) :266, + bias :270-271
 #pragma unroll
               for (int r = 0; r < 4; ++r) v[r] = round_to(v[r], XT);
               if (o < nvalid) {
@@ -435,7 +437,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64g_kernel(
 }  // namespace bcfft
 
 namespace {
-template <bool GLU>
+template <bool GLU, bool HB>
 void launch_dm64g(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt, void* y,
                   hipStream_t s) {
   const int groups = GLU ? (n_out + 15) / 16 : (n_out + 31) / 32;
@@ -445,7 +447,7 @@ void launch_dm64g(const void* x, int64_t n, int n_out, const void* spec, const v
   if (total > n_mtiles) total = n_mtiles;
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
   const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
-  hipLaunchKernelGGL((bcfft::bc_forward_dm64g_kernel<GLU>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_out,
+  hipLaunchKernelGGL((bcfft::bc_forward_dm64g_kernel<GLU, HB>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_out,
                      stat, osc, bias, bias_dt, y);
 }
 }  // namespace
@@ -462,7 +464,8 @@ bool dm64g_eligible(int n_in, int b, int xdt, bool yf32, int n_out, bool glu) {
 
 void launch_forward_dm64g(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt,
                           void* y, bool glu, hipStream_t s) {
-  if (glu) launch_dm64g<true>(x, n, n_out, spec, nullptr, BCFFT_NONE, y, s);
-  else launch_dm64g<false>(x, n, n_out, spec, bias, bias_dt, y, s);
+  if (glu) launch_dm64g<true, false>(x, n, n_out, spec, nullptr, BCFFT_NONE, y, s);
+  else if (bias_dt != BCFFT_NONE) launch_dm64g<false, true>(x, n, n_out, spec, bias, bias_dt, y, s);
+  else launch_dm64g<false, false>(x, n, n_out, spec, bias, bias_dt, y, s);
 }
 }  // namespace bcfft

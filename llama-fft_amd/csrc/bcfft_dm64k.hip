@@ -89,6 +89,9 @@ __device__ __forceinline__ uint32_t pk_umax(uint32_t m, uint32_t w) {
 }
 }  // namespace dm64k
 
+// HB: a bias is added (the runtime bias_dt then names its dtype); without one the store path is
+// straight-line (a runtime test per stored quad split stage 3 into hundreds of basic blocks)
+template <bool HB>
 __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_in, int n_out, const uint32_t* __restrict__ stat,
     const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
@@ -627,7 +630,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = hf ? fmaf(E[nt][r], ysc[nt], -os[r]) : fmaf(E[nt][r], ysc[nt], os[r]);
-          if (bias_dt != BCFFT_NONE) {              // .to(x dtype) :266, + bias :270-271
+          if (HB) {                                 // .to(x dtype) :266, + bias :270-271
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = round_to(v[r], XT);
             if (o < nvalid) {
@@ -743,8 +746,12 @@ void launch_forward_dm64k(const void* x, int64_t n, int n_in, int n_out, const v
   const int64_t total = group_grid(device_cu_count(), groups, n_mtiles);
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
   const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
-  hipLaunchKernelGGL(bc_forward_dm64k_kernel, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat, osc,
-                     bias, bias_dt, y);
+  if (bias_dt != BCFFT_NONE)
+    hipLaunchKernelGGL(bc_forward_dm64k_kernel<true>, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat, osc,
+                       bias, bias_dt, y);
+  else
+    hipLaunchKernelGGL(bc_forward_dm64k_kernel<false>, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat,
+                       osc, bias, bias_dt, y);
 }
 
 }  // namespace bcfft

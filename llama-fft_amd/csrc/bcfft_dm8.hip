@@ -50,7 +50,9 @@ __device__ __forceinline__ int xunit8(int ks, int f, int q) { return 4096 * ks +
 __device__ __forceinline__ int yunit8(int w, int o, int par) { return 4096 * par + 512 * w + 16 * o; }
 }  // namespace dm8
 
-template <bool GLU>
+// HB: a bias is added (the runtime bias_dt then names its dtype); without one the store path is
+// straight-line (a runtime test per stored quad split stage 3 into ~300 basic blocks)
+template <bool GLU, bool HB>
 __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_out, const uint32_t* __restrict__ stat,
     const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
@@ -444,7 +446,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
             float v[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = hf ? fmaf(E[nt][r], ysc[nt], -os[r]) : fmaf(E[nt][r], ysc[nt], os[r]);
-            if (bias_dt != BCFFT_NONE) {            // .to(x dtype) :266, + bias :270-271
+            if (HB) {                               // .to(x dtype) :266, + bias :270-271
 #pragma unroll
               for (int r = 0; r < 4; ++r) v[r] = round_to(v[r], XT);
               if (o < nvalid) {
@@ -570,7 +572,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
 }  // namespace bcfft
 
 namespace {
-template <bool GLU>
+template <bool GLU, bool HB>
 void launch_dm8(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt, void* y,
                 hipStream_t s) {
   const int groups = GLU ? (n_out + 15) / 16 : (n_out + 31) / 32;
@@ -579,7 +581,7 @@ void launch_dm8(const void* x, int64_t n, int n_out, const void* spec, const voi
   const int64_t total = bcfft::group_grid(bcfft::device_cu_count(), groups, n_mtiles);
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
   const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
-  hipLaunchKernelGGL((bcfft::bc_forward_dm8_kernel<GLU>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_out, stat,
+  hipLaunchKernelGGL((bcfft::bc_forward_dm8_kernel<GLU, HB>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_out, stat,
                      osc, bias, bias_dt, y);
 }
 }  // namespace
@@ -590,8 +592,9 @@ bool dm8_eligible(int n_in, int b, int xdt, bool yf32) { return dm_eligible(n_in
 
 void launch_forward_dm8(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt, void* y,
                         bool glu, hipStream_t s) {
-  if (glu) launch_dm8<true>(x, n, n_out, spec, nullptr, BCFFT_NONE, y, s);
-  else launch_dm8<false>(x, n, n_out, spec, bias, bias_dt, y, s);
+  if (glu) launch_dm8<true, false>(x, n, n_out, spec, nullptr, BCFFT_NONE, y, s);
+  else if (bias_dt != BCFFT_NONE) launch_dm8<false, true>(x, n, n_out, spec, bias, bias_dt, y, s);
+  else launch_dm8<false, false>(x, n, n_out, spec, bias, bias_dt, y, s);
 }
 }  // namespace bcfft
 

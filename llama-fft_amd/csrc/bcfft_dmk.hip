@@ -89,7 +89,9 @@ __device__ __forceinline__ uint32_t f16_pow2_neg(int d) {
 // SPL (decode / short-prefill sizes, bc_dmk_finish_kernel): the K-chunks are split into kz slices;
 // workgroup b takes slice b % kz of exactly one (group, tile) and writes its partial y in fp32 to
 // ws[slice][token][column] (no rounding, no bias), and a finishing pass sums the slices.
-template <int TT, bool SPL = false>
+// HB: a bias is added (the runtime bias_dt then names its dtype); without one the store path is
+// straight-line (a runtime test per stored quad split stage 3 into hundreds of basic blocks)
+template <int TT, bool SPL = false, bool HB = false>
 __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_in, int n_out, const uint32_t* __restrict__ stat,
     const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv,
@@ -505,7 +507,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
               *reinterpret_cast<float4*>(wsp + o * B + 16 * mt + 4 * g + 64 * hf) = make_float4(v[0], v[1], v[2], v[3]);
             continue;
           }
-          if (bias_dt != BCFFT_NONE) {              // .to(x dtype) :266, + bias :270-271
+          if (HB) {                                 // .to(x dtype) :266, + bias :270-271
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = round_to(v[r], XT);
             if (o < nvalid) {
@@ -712,12 +714,19 @@ void launch_forward_dmk(const void* x, int64_t n, int n_in, int n_out, const voi
 #endif
   const int64_t n_mtiles = t16 ? (n + 15) / 16 : (n + 7) / 8;
   const int64_t total = group_grid(cus, groups, n_mtiles);
-  if (t16)
-    hipLaunchKernelGGL((bc_forward_dmk_kernel<16, false>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out,
-                       stat, osc, bias, bias_dt, y, 1, nullptr);
+  const bool hb = bias_dt != BCFFT_NONE;
+  if (t16 && hb)
+    hipLaunchKernelGGL((bc_forward_dmk_kernel<16, false, true>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_in,
+                       n_out, stat, osc, bias, bias_dt, y, 1, nullptr);
+  else if (t16)
+    hipLaunchKernelGGL((bc_forward_dmk_kernel<16, false, false>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_in,
+                       n_out, stat, osc, bias, bias_dt, y, 1, nullptr);
+  else if (hb)
+    hipLaunchKernelGGL((bc_forward_dmk_kernel<8, false, true>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_in,
+                       n_out, stat, osc, bias, bias_dt, y, 1, nullptr);
   else
-    hipLaunchKernelGGL((bc_forward_dmk_kernel<8, false>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out,
-                       stat, osc, bias, bias_dt, y, 1, nullptr);
+    hipLaunchKernelGGL((bc_forward_dmk_kernel<8, false, false>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_in,
+                       n_out, stat, osc, bias, bias_dt, y, 1, nullptr);
 }
 
 // the split form's finishing pass: y = (sum over the kz slices in order, rounded to bf16) + bias,

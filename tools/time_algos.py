@@ -96,6 +96,9 @@ if __name__ == "__main__":
         shapes = ([(4096, 4096, 64, "fp32", n) for n in (1, 16, 64, 128, 256, 512, 1024)]
                   + [(4096, 4096, 128, io, n) for io in ("fp32", "bf16") for n in (1, 16, 64, 128, 256, 512, 1024)]
                   + [(4096, 11008, 128, "bf16", n) for n in (20, 128, 256, 512)])
+    if "--bf16all" in sys.argv:                     # every bf16 DFT kernel at the sweep's N = 8192 shapes
+        shapes = [(k, m, b, "bf16", 8192) for b in (128, 64, 256)
+                  for k, m in ((4096, 4096), (4096, 11008), (11008, 4096))]
     if "--smalln" in sys.argv:                      # AUTO's small-N crossover
         shapes = [(4096, 4096, b, io, n) for b in (64, 128) for io in ("fp32",) for n in (16, 64, 128, 256, 512, 1024, 2048)]
     for k, m, b, io, n in shapes:
