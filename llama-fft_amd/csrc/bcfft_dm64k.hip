@@ -729,7 +729,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
   char* yreg = lds + (rsel ^ 1) * REGION;
   stage3(yreg, wave, wrr[wave], mprev >= 0 ? mprev * TT + wave : -1);
   stage3(yreg, wave + 8, wrr[wave + 8], mprev >= 0 ? mprev * TT + wave + 8 : -1);
-  wait_vmcnt<0>();                                  // the last step's empty-range B loads
+  // the last step's empty-range B loads: waited for with the fragments as operands, so that their
+  // registers stay reserved (not reused by ywrite / stage 3) until the loads have returned
+  wait_b(std::integral_constant<int, 0>{}, breg);
 }
 
 #undef DST

@@ -364,21 +364,28 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
     }
     const __amdgpu_buffer_rsrc_t nbrs = b_rsrc(cn);
     const int vo = opaque(lane) * 16;
+    // A rows of bin fb for the MT M-tiles; the next bin's are read while this bin's are scaled and
+    // multiplied (issued above the per-bin load branch, so the LDS latency is off the chain)
+    auto a_off = [&](int fb, int mt) { return 8 * XSLOT * mt + 64 * (fb ^ ((fb >> 2) & 1)); };
+    uint4 araw[2][MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) araw[0][mt] = *reinterpret_cast<const uint4*>(ab + a_off(0, mt));
+    const bool bin0 = wave == 0;                    // bin 0 (wave 0, fb 0): (X_0, X_64), no swap
 #pragma unroll
     for (int fb = 0; fb < BPW; ++fb) {
-      const int f = wave * BPW + fb;
+      if (fb + 1 < BPW) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) araw[(fb + 1) & 1][mt] = *reinterpret_cast<const uint4*>(ab + a_off(fb + 1, mt));
+      }
+      const uint32_t sel = (fb == 0 && bin0) ? 0x03020100u : a_sel;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        uint4 raw = *reinterpret_cast<const uint4*>(ab + 8 * XSLOT * mt + 64 * (fb ^ ((fb >> 2) & 1)));
-        if (f == 0) {
-          raw.x = pkmul(raw.x, amul0[mt]); raw.y = pkmul(raw.y, amul0[mt]);
-          raw.z = pkmul(raw.z, amul0[mt]); raw.w = pkmul(raw.w, amul0[mt]);
-        } else {
-          raw.x = pkmul(__builtin_amdgcn_perm(raw.x, raw.x, a_sel), amul[mt]);
-          raw.y = pkmul(__builtin_amdgcn_perm(raw.y, raw.y, a_sel), amul[mt]);
-          raw.z = pkmul(__builtin_amdgcn_perm(raw.z, raw.z, a_sel), amul[mt]);
-          raw.w = pkmul(__builtin_amdgcn_perm(raw.w, raw.w, a_sel), amul[mt]);
-        }
+        const uint32_t mul = (fb == 0 && bin0) ? amul0[mt] : amul[mt];
+        uint4 raw = araw[fb & 1][mt];
+        raw.x = pkmul(__builtin_amdgcn_perm(raw.x, raw.x, sel), mul);
+        raw.y = pkmul(__builtin_amdgcn_perm(raw.y, raw.y, sel), mul);
+        raw.z = pkmul(__builtin_amdgcn_perm(raw.z, raw.z, sel), mul);
+        raw.w = pkmul(__builtin_amdgcn_perm(raw.w, raw.w, sel), mul);
         const f16x8 a = __builtin_bit_cast(f16x8, raw);
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
