@@ -143,7 +143,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
   // ---- stage 1 (wave w, token slot w): x rows -> X units (one fp16 term), in place, per half.
   // xwait: this wave's x DMA of the token is in flight (pieces 0-3 = half 0, behind its older y
   // stores): wait for half 0 alone, then for half 1 after half 0's transform
-  auto stage1 = [&](char* region, int par, int sl, bool xwait = false) {
+  // XOFF: VMEM operations issued after the x DMA this wave waits for (the stage-3-first order
+  // below has issued its 8 y stores and the next tile's 8 DMA pieces by then)
+  auto stage1 = [&](char* region, int par, int sl, bool xwait, auto xoff_c) {
+    constexpr int XOFF = decltype(xoff_c)::value;
     const int l = opaque(lane);
     const int b16 = l & 15, g = l >> 4;
     char* slot = region + sl * SLOT;
@@ -209,8 +212,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
       if (l == 0) wsc[par * 16 + sl * 2 + h] = sx - 7;
 #else
       if (xwait) {
-        if (h == 0) wait_vmcnt<NDMA / 2>();
-        else wait_vmcnt<0>();
+        if (h == 0) wait_vmcnt<NDMA / 2 + XOFF>();
+        else wait_vmcnt<XOFF>();
       }
       // x of blocks 16h + b16: t = 32 ks + 8 g + j and t + 64 (j < 8); the half's x rows are
       // exactly the bytes its X units replace
@@ -517,15 +520,15 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
     if (it == 0) {                                  // fill: token w (x streamed by wave w)
       if (have) {
         wait_vmcnt<0>();
-        stage1(region, par, wave);
+        stage1(region, par, wave, false, std::integral_constant<int, 0>{});
       }
     } else if (!have) {                             // drain: token w of the last tile
       stage3(other, par ^ 1, m - gstride, wave);
     } else if (fwave) {
       wait_vmcnt<0>();                              // this wave's own x DMA (both slots)
       STAMP(sb + 1);
-      stage1(region, par, wave);
-      stage1(region, par, wave + 4);
+      stage1(region, par, wave, false, std::integral_constant<int, 0>{});
+      stage1(region, par, wave + 4, false, std::integral_constant<int, 0>{});
     } else {
       stage3(other, par ^ 1, m - gstride, wave - 4);
       stage3(other, par ^ 1, m - gstride, wave);
@@ -541,21 +544,40 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
     }
     stage2(region, par);
 #else
-    if (have) {
-#if defined(BCFFT_S1_ILP) || (defined(BCFFT_DM8_XWAIT) && BCFFT_DM8_XWAIT == 0)
-      wait_vmcnt<0>();                              // this wave's x (and its older y stores)
-      STAMP(sb + 1);
-      stage1(region, par, wave);
-#else
-      STAMP(sb + 1);
-      stage1(region, par, wave, true);              // waits per half for this wave's x (and its older y stores)
+#ifndef BCFFT_DM8_MIX
+#define BCFFT_DM8_MIX 1
 #endif
-    }
-    STAMP(sb + 2);
-    if (it > 0) stage3(other, par ^ 1, m - gstride, wave);
-    if (m + gstride < n_mtiles) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
-      dma_token(m + gstride, other, wave);
+    // waves 0-3 run stage 3 and the next tile's x DMA before their stage 1, waves 4-7 after it:
+    // each SIMD then pairs a memory-heavy wave with a transform-heavy one, and the 64 DMA pieces
+    // of the CU issue in two bursts half a phase apart instead of one
+    if (BCFFT_DM8_MIX && wave < 4 && it > 0 && have) {
+      STAMP(sb + 1);
+      stage3(other, par ^ 1, m - gstride, wave);
+      STAMP(sb + 2);
+      if (m + gstride < n_mtiles) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
+        dma_token(m + gstride, other, wave);
+        stage1(region, par, wave, true, std::integral_constant<int, (GLU ? 4 : 8) + NDMA>{});   // stores, DMA
+      } else {
+        stage1(region, par, wave, true, std::integral_constant<int, GLU ? 4 : 8>{});          // stores
+      }
+    } else {
+      if (have) {
+#if defined(BCFFT_S1_ILP) || (defined(BCFFT_DM8_XWAIT) && BCFFT_DM8_XWAIT == 0)
+        wait_vmcnt<0>();                              // this wave's x (and its older y stores)
+        STAMP(sb + 1);
+        stage1(region, par, wave, false, std::integral_constant<int, 0>{});
+#else
+        STAMP(sb + 1);
+        stage1(region, par, wave, true, std::integral_constant<int, 0>{});   // waits per half for this wave's x (and its older y stores)
+#endif
+      }
+      STAMP(sb + 2);
+      if (it > 0) stage3(other, par ^ 1, m - gstride, wave);
+      if (m + gstride < n_mtiles) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
+        dma_token(m + gstride, other, wave);
+      }
     }
     STAMP(sb + 3);
     if (!have) break;
