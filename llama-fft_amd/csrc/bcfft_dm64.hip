@@ -389,14 +389,32 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64_kernel(
     char* other = lds + ((it + 1) & 1) * REGION;
     const int par = it & 1;
     const bool have = m < n_mtiles;
-    if (have) {
-      wait_vmcnt<0>();                              // this wave's x (and its older y stores)
+#ifndef BCFFT_DM64_MIX
+#define BCFFT_DM64_MIX 1
+#endif
+    // waves 0-3 run stage 3 and the next tile's x DMA before their stage 1 (bcfft_dm8.hip's mixed
+    // order: a memory-heavy and a transform-heavy wave per SIMD, two DMA bursts per phase)
+    if (BCFFT_DM64_MIX && wave < 4 && it > 0 && have) {
+      constexpr int NST = GLU ? 2 : 4;              // stage 3's stores
+      stage3(other, par ^ 1, m - gstride);
+      if (m + gstride < n_mtiles) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
+        dma_token(m + gstride, other);
+        wait_vmcnt<NST + NDMA>();                   // this wave's x (older than the stores and the DMA)
+      } else {
+        wait_vmcnt<NST>();
+      }
       stage1(region, par);
-    }
-    if (it > 0) stage3(other, par ^ 1, m - gstride);
-    if (m + gstride < n_mtiles) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
-      dma_token(m + gstride, other);
+    } else {
+      if (have) {
+        wait_vmcnt<0>();                            // this wave's x (and its older y stores)
+        stage1(region, par);
+      }
+      if (it > 0) stage3(other, par ^ 1, m - gstride);
+      if (m + gstride < n_mtiles) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
+        dma_token(m + gstride, other);
+      }
     }
     if (!have) break;
     lds_barrier();                                  // Ba: X units and scales complete
