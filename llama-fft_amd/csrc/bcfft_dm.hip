@@ -806,21 +806,24 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
     // it before Bb. FILL_SPLIT / DRAIN_SPLIT: see the kernel's top.
     const bool early = EARLY_X && it == 0 && !fwave && m + gstride < n_mtiles;
     if (early) dma_token(m + gstride, other, 0, NDMA);
-    if (FILL_SPLIT && it == 0) {                    // fill: both waves of a slot, one half each
-      if (have_f) {
+    // stage 1 has ONE call site: the fill (each wave of a slot one half) runs the same code as the
+    // steady state, so its instruction fetch warms the F waves' stage 1 of iteration 1 (with two
+    // inlined copies, the first steady-state stage 1 of every CU missed the instruction cache
+    // together: ~5 k cycles, profiles/r05y_timeline_dm_nofd.txt)
+    const bool fill = FILL_SPLIT && it == 0;
+    constexpr bool XW = BCFFT_DM_XWAIT != 0 && ES == 4 && EP == 0;
+    if (have_f && (fill || fwave)) {
+      if (fill) {                                   // fill: both waves of a slot, one half each
         if (!fwave && early) wait_vmcnt<NPIECE + NDMA>();   // own half of tile 0's x (prologue)
         else wait_vmcnt<NPIECE>();
-        stage1(region, par, fwave ? 1 : 2);
-      }
-    } else if (fwave) {
-      if (have_f) {
-        constexpr bool XW = BCFFT_DM_XWAIT != 0 && ES == 4 && EP == 0;
+      } else {
         if (LATE_W && it == 0) wait_vmcnt<NPIECE>();   // tile 0's x, not the weight loads behind it
         else if (!XW) wait_vmcnt<0>();              // this wave's own x DMA (issued a phase ahead)
-        stage1(region, par, 3, XW && it > 0);
-      } else if (DRAIN_SPLIT) {                     // drain: the last tile's stage 3, N-tile 1
-        stage3(other, par ^ 1, m - gstride, std::integral_constant<int, 2>{});
       }
+      stage1(region, par, fill ? (fwave ? 1 : 2) : 3, !fill && XW && it > 0);
+    } else if (fwave) {
+      if (!have_f && DRAIN_SPLIT)                   // drain: the last tile's stage 3, N-tile 1
+        stage3(other, par ^ 1, m - gstride, std::integral_constant<int, 2>{});
     } else if (it > 0) {
       if (DRAIN_SPLIT && !have_f) stage3(other, par ^ 1, m - gstride, std::integral_constant<int, 1>{});
       else stage3(other, par ^ 1, m - gstride, std::integral_constant<int, 3>{});

@@ -65,6 +65,11 @@ def run(m, io, n, k=4096, b=128):
         sel = wv == w
         med = [np.median(seg[sel][:, 1:-1, j]) for j in range(5)] if tiles > 2 else [0] * 5
         print(f"wave {w}    " + " ".join(f"{v:10.0f}" for v in med))
+    for it in range(tiles):                      # per iteration (iteration 4 carries the sub-phase stamps)
+        row = []
+        for name, sel in (("F", wv < 4), ("I", wv >= 4)):
+            row.append(name + " " + " ".join(f"{np.median(seg[sel][:, it, j]):6.0f}" for j in range(5)))
+        print(f"  it {it}: " + "   ".join(row))
     if tiles > 4:                                # sub-phases of iteration 4 (from its loop top)
         top = st[:, 1 + 6 * 4]
         fsub = ["dma wait", "h0 rd+max", "h0 mfma", "h0 X wr", "h1 rd+max", "h1 mfma", "h1 X wr", "-"]
