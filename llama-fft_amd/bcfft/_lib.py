@@ -77,6 +77,9 @@ _SIGNATURES = {
 
 _lib = None
 _native = None
+# the operators' handles (OpOverload), looked up once: torch.ops attribute access costs ~1 us a call
+NATIVE_FORWARD = None
+NATIVE_FORWARD_GLU = None
 _lock = threading.RLock()
 # torch.ops.bcfft_native (csrc/bcfft_torch.cpp): the C++ operators over this ABI, built next to it
 TORCH_OP_PATH = os.path.join(os.path.dirname(LIB_PATH), "libbcfft_torch.so")
@@ -113,7 +116,7 @@ def native_op() -> bool:
     when the library is present but does not load (e.g. built against another torch: undefined
     c10 symbols), which warns once. Either way the kernels are libbcfft.so's (the ctypes path
     calls the same ABI): there is no CPU path."""
-    global _native
+    global _native, NATIVE_FORWARD, NATIVE_FORWARD_GLU
     if _native is None:
         with _lock:
             if _native is None:
@@ -128,6 +131,9 @@ def native_op() -> bool:
                         warnings.warn(f"{TORCH_OP_PATH} did not load ({e}); bcfft calls libbcfft.so through "
                                       "ctypes instead. Rebuild with `make -C llama-fft_amd`.", RuntimeWarning)
                         ok = False
+                if ok:
+                    NATIVE_FORWARD = torch.ops.bcfft_native.forward.default
+                    NATIVE_FORWARD_GLU = torch.ops.bcfft_native.forward_glu.default
                 _native = ok
     return _native
 
@@ -153,7 +159,7 @@ def stream_handle(device: torch.device) -> int:
 
 
 def require_device(t: torch.Tensor, what: str) -> None:
-    if t.device.type != "cuda":
+    if not t.is_cuda:
         raise RuntimeError(
             f"{what}: the MI355X BC engine runs on ROCm device tensors only (got {t.device}); "
             "move the module and inputs to the GPU. There is no CPU path in the product.")

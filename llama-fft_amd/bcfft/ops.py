@@ -6,6 +6,7 @@ and again in the library (status codes).
 """
 from __future__ import annotations
 
+import os
 import torch
 
 from . import _lib
@@ -91,7 +92,7 @@ def forward_glu(x2d: torch.Tensor, spec_gu: torch.Tensor, block_size: int, gate_
                          "(auto, stationary, dft, dftx); run gate and up as two forwards instead")
     _lib.require_device(x2d, "bcfft.forward_glu")
     if _lib.native_op():
-        return torch.ops.bcfft_native.forward_glu(x2d, spec_gu, block_size, gate_features, _lib.ALGOS[algo])
+        return _lib.NATIVE_FORWARD_GLU(x2d, spec_gu, block_size, gate_features, _lib.ALGOS[algo])
     n, k = x2d.shape
     if block_size > 0 and gate_features % block_size == 0 and k % block_size == 0:
         _check_spectra(spec_gu, 32 * (-(-(gate_features // block_size) // 16)), k // block_size, block_size,
@@ -188,7 +189,6 @@ def glu_eligible(in_features: int, block_size: int, dtype: torch.dtype | None = 
 
 def default_algo() -> str:
     """BCFFT_ALGO env var: auto (default) | dft | dftx | dftp | stationary | mfma | valu."""
-    import os
     a = os.environ.get("BCFFT_ALGO", "auto").lower()
     if a not in _lib.ALGOS:
         raise ValueError(f"BCFFT_ALGO={a!r}: expected one of {sorted(_lib.ALGOS)}")
@@ -201,7 +201,6 @@ def precise_mode() -> bool:
     times its cancellation), the split-bf16 MFMA kernel (~1e-5) at other b <= 128, fp32 VALU above.
     The default AUTO keeps the faster dftx / stationary engines (~3e-4, per token up to ~6e-3 on
     near-cancelling tokens); 16-bit activations are unaffected (their output rounding dominates)."""
-    import os
     return os.environ.get("BCFFT_PRECISE", "0") not in ("", "0")
 
 
@@ -228,7 +227,7 @@ def forward(x2d: torch.Tensor, spec: torch.Tensor, bias: torch.Tensor | None, bl
     _lib.require_device(x2d, "bcfft.forward")
     algo = resolve_algo(algo, x2d.dtype, block_size, x2d.shape[-1])
     if _lib.native_op():                         # the same call as one C++ op (csrc/bcfft_torch.cpp)
-        return torch.ops.bcfft_native.forward(x2d, spec, bias, block_size, out_features, _lib.ALGOS[algo], split_k)
+        return _lib.NATIVE_FORWARD(x2d, spec, bias, block_size, out_features, _lib.ALGOS[algo], split_k)
     n, k = x2d.shape
     if block_size > 0 and out_features % block_size == 0 and k % block_size == 0:
         _check_spectra(spec, out_features // block_size, k // block_size, block_size, "bcfft.forward")
