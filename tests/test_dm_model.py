@@ -5,6 +5,7 @@ parity tolerance, before any GPU run."""
 import numpy as np
 import pytest
 
+import dm_model as DM
 from dm_model import dm_forward, dm_table
 from oracle import bc_oracle as orc
 
@@ -102,3 +103,73 @@ def test_precise_model_vs_oracle(scale):
         assert r < 8e-5, (t, r)
     partial = dm_forward(x, c, precise=True, terms=(1, 0, 1))   # no weight residual: dftx-like
     assert np.linalg.norm(partial - ref) / np.linalg.norm(ref) > 3 * rel
+
+
+def _table_words(name, count):
+    text = open(DM._TABLE).read()
+    body = text[text.index(f"{name}[{count}]"):]
+    body = body[:body.index("};")]
+    return np.array([int(w, 16) for w in __import__("re").findall(r"0x([0-9a-f]{8})u", body)], dtype=np.uint32)
+
+
+def _bf16(bits):
+    return (bits.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+
+
+def test_dm64k_bf16_fragments_are_the_dft():
+    """kDmB64 (bcfft_dm64k.hip's stage-1 A fragments, [pr][mt][term][lane][8] bf16): hi + lo of the
+    b = 64 even / odd DFT columns times 2^-7 to ~2^-17, hi the RNE bf16 of each entry, and the
+    fragment layout A[m = lane & 15][k = 8 (lane >> 4) + e] = column 32 pr + 16 mt + m, row t = k."""
+    w = _table_words("kDmB64", 2048).reshape(2, 2, 2, 64, 4)
+    el = np.empty((2, 2, 2, 64, 8))
+    el[..., 0::2] = _bf16(w & 0xFFFF)
+    el[..., 1::2] = _bf16(w >> 16)
+    t = np.arange(32)
+    F = np.zeros((32, 64))
+    F[:, 0], F[:, 1] = 1.0, (-1.0) ** t
+    for j in range(1, 16):
+        F[:, 2 * j], F[:, 2 * j + 1] = np.cos(2 * np.pi * j * t / 32), -np.sin(2 * np.pi * j * t / 32)
+    for j in range(16):
+        th = 2 * np.pi * (2 * j + 1) * t / 64
+        F[:, 32 + 2 * j], F[:, 32 + 2 * j + 1] = np.cos(th), -np.sin(th)
+    ref = F * 2.0 ** -7
+    for pr in range(2):
+        for mt in range(2):
+            for ln in range(64):
+                col, ts = 32 * pr + 16 * mt + (ln & 15), 8 * (ln >> 4) + np.arange(8)
+                hi, lo = el[pr, mt, 0, ln], el[pr, mt, 1, ln]
+                np.testing.assert_allclose(hi + lo, ref[ts, col], rtol=0, atol=2.0 ** -24)
+                # hi is bf16(v): |v - hi| within half a bf16 ulp of v (8 significant bits)
+                assert np.all(np.abs(ref[ts, col] - hi) <= 2.0 ** -8 * np.abs(ref[ts, col]) + 1e-30)
+
+
+def test_dm64k_direct_stage1_model():
+    """The direct stage 1 of bcfft_dm64k.hip in numpy: X = (F_hi + F_lo) x over all 64 points
+    (x_{t+32} negated for the odd bins), then X 2^sx rounded once to fp16, equals the exact
+    64-point rfft of the bf16 x to the fp16 rounding of X (the even / odd fp16 form it replaces
+    also rounds a, d and the table: its error is larger)."""
+    rng = np.random.default_rng(3)
+    w = _table_words("kDmB64", 2048).reshape(2, 2, 2, 64, 4)
+    el = np.empty((2, 2, 2, 64, 8))
+    el[..., 0::2] = _bf16(w & 0xFFFF)
+    el[..., 1::2] = _bf16(w >> 16)
+    A = np.zeros((64, 32))                            # [column][t]: hi + lo
+    for pr in range(2):
+        for mt in range(2):
+            for ln in range(64):
+                A[32 * pr + 16 * mt + (ln & 15), 8 * (ln >> 4) + np.arange(8)] = el[pr, mt, 0, ln] + el[pr, mt, 1, ln]
+    x = rng.standard_normal((16, 64)).astype(np.float32)
+    xb = _bf16(x.view(np.uint32) >> 16)               # bf16 truncation: any bf16 input
+    Xs = np.zeros((16, 64))
+    Xs[:, :32] = (xb[:, :32] + xb[:, 32:]) @ A[:32].T     # even columns: x_{t+32} as is
+    Xs[:, 32:] = (xb[:, :32] - xb[:, 32:]) @ A[32:].T     # odd columns: x_{t+32} negated
+    Xs *= 2.0 ** 7
+    full = np.fft.rfft(xb, axis=1)                   # bins 0..32
+    ref = np.zeros((16, 64))
+    ref[:, 0], ref[:, 1] = full[:, 0].real, full[:, 32].real
+    for j in range(1, 16):
+        ref[:, 2 * j], ref[:, 2 * j + 1] = full[:, 2 * j].real, full[:, 2 * j].imag
+    for j in range(16):
+        ref[:, 32 + 2 * j], ref[:, 32 + 2 * j + 1] = full[:, 2 * j + 1].real, full[:, 2 * j + 1].imag
+    err = np.abs(Xs - ref).max() / np.abs(ref).max()
+    assert err < 2.0 ** -15, err
