@@ -573,8 +573,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256k_kernel(
   const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint32_t*>(stat + 4) + ((int64_t)((grp_o >> 1) * NW + wave) * npiece) * 256, 0, npiece * 1024,
       0x00020000);
-  auto load_b1 = [&](int c, int fb, u32x4 (&breg)[BPW]) {
-    const int vo = opaque(lane) * 16 + (c * 2 + (grp_o & 1)) * 1024;
+  // live = false: an empty-range load (the offset lies past the buffer: zeros, no memory access)
+  auto load_b1 = [&](int c, int fb, u32x4 (&breg)[BPW], bool live = true) {
+    const int vo = opaque(lane) * 16 + (live ? (c * 2 + (grp_o & 1)) * 1024 : npiece * 1024);
     asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen"
                  : "=v"(breg[fb]) : "v"(vo), "s"(brs), "s"(fb * KS * 2048));
   };
@@ -786,26 +787,29 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256k_kernel(
     const uint32_t amul0 = a_reim ? (h0 << 16) : h0;
     const char* ab = region + a_t * SLOT + 16 * kb;
     // B of this step: the younger VMEM is this step's x DMA and, at a tile's first chunk, the
-    // previous tile's stage-3 stores before it
-    if (tile0) wait_b(std::integral_constant<int, 8 + NDMA_C>{}, breg);
-    else wait_b(std::integral_constant<int, NDMA_C>{}, breg);
-    const int nc = nb < 0 ? 0 : nb;
+    // previous tile's stage-3 stores before it. One operand-carrying wait on every path (one per
+    // branch made the compiler copy the 16 fragments where the paths joined)
+    if (!tile0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA_C) : "memory");
+    wait_b(std::integral_constant<int, 8 + NDMA_C>{}, breg);
+    const bool more = nb >= 0;
+    const int nc = more ? nb : 0;
+    // A rows one bin ahead (the LDS latency off the MFMA chain); bin 0 (wave 0, fb 0) branch-free
+    const bool bin0 = wave == 0;
+    uint4 anext = *reinterpret_cast<const uint4*>(ab + xunit(wave * BPW, 0));
 #pragma unroll
     for (int fb = 0; fb < BPW; ++fb) {
       const int k = wave * BPW + fb;
-      uint4 raw = *reinterpret_cast<const uint4*>(ab + xunit(k, 0));
-      if (k == 0) {
-        raw.x = pkmul(raw.x, amul0); raw.y = pkmul(raw.y, amul0);
-        raw.z = pkmul(raw.z, amul0); raw.w = pkmul(raw.w, amul0);
-      } else {
-        raw.x = pkmul(__builtin_amdgcn_perm(raw.x, raw.x, a_sel), amul);
-        raw.y = pkmul(__builtin_amdgcn_perm(raw.y, raw.y, a_sel), amul);
-        raw.z = pkmul(__builtin_amdgcn_perm(raw.z, raw.z, a_sel), amul);
-        raw.w = pkmul(__builtin_amdgcn_perm(raw.w, raw.w, a_sel), amul);
-      }
+      uint4 raw = anext;
+      if (fb + 1 < BPW) anext = *reinterpret_cast<const uint4*>(ab + xunit(k + 1, 0));
+      const uint32_t sel = (fb == 0 && bin0) ? 0x03020100u : a_sel;
+      const uint32_t mul = (fb == 0 && bin0) ? amul0 : amul;
+      raw.x = pkmul(__builtin_amdgcn_perm(raw.x, raw.x, sel), mul);
+      raw.y = pkmul(__builtin_amdgcn_perm(raw.y, raw.y, sel), mul);
+      raw.z = pkmul(__builtin_amdgcn_perm(raw.z, raw.z, sel), mul);
+      raw.w = pkmul(__builtin_amdgcn_perm(raw.w, raw.w, sel), mul);
       acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, raw),
                                                        __builtin_bit_cast(f16x8, breg[fb]), acc[fb], 0, 0, 0);
-      if (nb >= 0) load_b1(nc, fb, breg);
+      load_b1(nc, fb, breg, more);                  // past the last step: an empty-range load
     }
   };
 
@@ -995,6 +999,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256k_kernel(
     c = cn;
   }
   stage3(lds + (rsel ^ 1) * REGION, wrr[wave], mprev >= 0 ? mprev * TT + wave : -1);
+  // the last step's empty-range B loads: waited for with the fragments as operands, so their
+  // registers are not reused by ywrite / stage 3 while the loads are in flight
+  wait_b(std::integral_constant<int, 0>{}, breg);
 }
 
 // ---- weight image at b = 256: the generic STAT image kernels instantiated for B = 256 (groups
