@@ -27,6 +27,7 @@ CASES = [
     (4160, 2048, 300, True),    # 65 blocks: 2 chunks + 1 block (an odd K-step count)
     (16320, 1024, 19, False),   # 255 blocks: the largest K
     (8192, 11008, 64, False),   # 172 output blocks: 6 groups, the last partial
+    (4160, 2048, 8200, True),   # bias, two or three tiles per workgroup (HB path, empty-range B loads)
 ]
 
 
