@@ -502,6 +502,11 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256_kernel(
 // head = 4 scheme); otherwise bc_forward_dm256_kernel's.
 namespace d256 {
 constexpr int HEAD = 4;
+// wave priority falling through stage 1 (1) and stage 2 (2): set_prio, bcfft_dm64k.hip's finding
+#ifndef BCFFT_DM256K_PRIO
+#define BCFFT_DM256K_PRIO 3
+#endif
+constexpr int PRIO = BCFFT_DM256K_PRIO;
 constexpr int SC2_OFF = CS_OFF + 1024;              // chunk scale exponents [8 tokens]
 constexpr int RR_OFF = SC2_OFF + 64;                // per-token reference exponents [8]
 constexpr int OS2_OFF = RR_OFF + 64;                // the workgroup's 16 inverse weight scales
@@ -620,6 +625,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256k_kernel(
     const int cx = (p4 >> 1) ^ fsw(8 * g + q4);
     const int trb = F_OFF + 256 * (8 * g + q4) + 8 * (p4 & 1);
     const char* rowp = slot + b16 * (B * ES);
+    if constexpr ((PRIO & 1) != 0) set_prio(2);
     uint32_t xr[4][2][4];
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt)
@@ -701,6 +707,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256k_kernel(
           *reinterpret_cast<uint32_t*>(slot + xunit(2 * f + 4, 0) + 4 * b16) = pk_rne(acc8[4 * pr + mt][2], acc8[4 * pr + mt][3]);
         }
     }
+    if constexpr ((PRIO & 1) != 0) set_prio(1);
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) {
       f32x4 accp[4], accq[4];
@@ -798,6 +805,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256k_kernel(
     uint4 anext = *reinterpret_cast<const uint4*>(ab + xunit(wave * BPW, 0));
 #pragma unroll
     for (int fb = 0; fb < BPW; ++fb) {
+      if constexpr ((PRIO & 2) != 0) set_prio(3 - 4 * fb / BPW);
       const int k = wave * BPW + fb;
       uint4 raw = anext;
       if (fb + 1 < BPW) anext = *reinterpret_cast<const uint4*>(ab + xunit(k + 1, 0));

@@ -59,6 +59,14 @@ constexpr int LDS_BYTES = TB_OFF + 8192;
 constexpr int FRAGS = BW * KC * NT;                 // B fragments per wave and chunk
 constexpr int NDMA = 2 * 4;                         // 1-KiB x DMA pieces per wave and chunk (2 tokens)
 constexpr int HEAD = 4;
+// wave priority falling with the work done in stage 1 (1) and stage 2 (2) (s_setprio, 0 = lowest):
+// waves 4-7, younger than their SIMD partners 0-3, lose every age-ordered arbitration and finished
+// both stages ~1.1 k cycles later; with the priority a wave that is behind issues first (117.7 vs
+// 119.6 us at N = 8192, profiles/r05ll_ab_dm64k_prio.log). -DBCFFT_DM64K_PRIO=0 builds without
+#ifndef BCFFT_DM64K_PRIO
+#define BCFFT_DM64K_PRIO 3
+#endif
+constexpr int PRIO = BCFFT_DM64K_PRIO;
 // analysis builds only (results are WRONG when set): 1 no B loads, 2 no stage-1 arithmetic, 4 no
 // stage-2 MFMAs, 8 no stage 3, 16 no x DMA, 32 no y stores
 #ifdef BCFFT_DM64K_ABL
@@ -213,6 +221,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
     int xwb[2];
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) xwb[pr] = 256 * g + 64 * (pr ^ (g & 1)) + 4 * b16;
+    if constexpr ((PRIO & 1) != 0) __builtin_amdgcn_s_setprio(2);
 #pragma unroll 1
     for (int t2 = 0; t2 < 2; ++t2) {
       const int tl = wave + 8 * t2;
@@ -271,6 +280,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
             *reinterpret_cast<uint32_t*>(xb + xwb[pr] + 1024 * mt + 128) = pk_scaled(v[2], v[3], S);
           }
       }
+      if constexpr ((PRIO & 1) != 0) __builtin_amdgcn_s_setprio(1);
     }
   };
 #else
@@ -498,6 +508,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
     const bool bin0 = wave == 0;                    // bin 0 (wave 0, fb 0): (X_0, X_32), no swap
 #pragma unroll
     for (int fb = 0; fb < BW; ++fb) {
+      if constexpr ((PRIO & 2) != 0) set_prio(3 - fb);
       if (fb + 1 < BW) {
 #pragma unroll
         for (int j = 0; j < KC; ++j)

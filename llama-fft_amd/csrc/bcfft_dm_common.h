@@ -58,5 +58,14 @@ __device__ __forceinline__ uint32_t wave_umax(uint32_t v) {
 __device__ __forceinline__ f16x8 frag(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   return __builtin_bit_cast(f16x8, make_uint4(a, b, c, d));
 }
+// s_setprio(p) for a p the unrolled loops fold to a constant (the instruction takes an immediate).
+// The streamed-weight kernels lower a wave's priority as it works through a stage, so that of
+// the two waves on a SIMD the one behind issues first instead of the older one (bcfft_dm64k.hip)
+__device__ __forceinline__ void set_prio(int p) {
+  if (p >= 3) __builtin_amdgcn_s_setprio(3);
+  else if (p == 2) __builtin_amdgcn_s_setprio(2);
+  else if (p == 1) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+}
 }  // namespace dmh
 }  // namespace bcfft

@@ -53,6 +53,11 @@ constexpr int ABL = BCFFT_DMK_ABL;
 #else
 constexpr int ABL = 0;
 #endif
+// wave priority falling through stage 1 (1) and stage 2 (2): set_prio, bcfft_dm64k.hip's finding
+#ifndef BCFFT_DMK_PRIO
+#define BCFFT_DMK_PRIO 3
+#endif
+constexpr int PRIO = BCFFT_DMK_PRIO;
 
 constexpr int B = 128, NW = 8, BPW = 8, NT = 2, NOG = 32;
 constexpr int XSLOT = 4096 + 64;                    // one token's 16-block x chunk -> X units
@@ -216,6 +221,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
     const int q4 = (l & 15) >> 2, p4 = l & 3;
     const int cx = (p4 >> 1) ^ fsw(8 * g + q4);
     const int trb = F_OFF + 256 * (8 * g + q4) + 8 * (p4 & 1);
+    if constexpr ((PRIO & 1) != 0) set_prio(2);
 #pragma unroll 1
     for (int t2 = 0; t2 < TPW; ++t2) {
       char* slot = region + (TPW * wave + t2) * XSLOT;
@@ -284,6 +290,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
           *reinterpret_cast<uint32_t*>(slot + xwb + 1024 * mt + 128) = pk_rne(acc4[mt][2], acc4[mt][3]);
         }
       }
+      if constexpr ((PRIO & 1) != 0) set_prio(1);
     }
   };
 
@@ -373,6 +380,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
     const bool bin0 = wave == 0;                    // bin 0 (wave 0, fb 0): (X_0, X_64), no swap
 #pragma unroll
     for (int fb = 0; fb < BPW; ++fb) {
+      if constexpr ((PRIO & 2) != 0) set_prio(3 - 4 * fb / BPW);
       if (fb + 1 < BPW) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) araw[(fb + 1) & 1][mt] = *reinterpret_cast<const uint4*>(ab + a_off(fb + 1, mt));

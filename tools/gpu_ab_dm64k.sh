@@ -3,7 +3,7 @@
 TAG=$1; shift
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/$TAG || exit 1
 timeout -k 10 300 python -u -m pytest tests/test_gpu_dm64k.py -m gpu -x -v --timeout 150 --timeout-method thread > gpurun_out/$TAG/pytest_dm64k.log 2>&1 || { tail -30 gpurun_out/$TAG/pytest_dm64k.log; exit 1; }
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   for lib in "$@"; do
     case $lib in *st_*) continue;; esac
     echo "== $lib (pass $rep)"

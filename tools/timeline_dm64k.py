@@ -63,6 +63,16 @@ def main():
         print(f"-- chunk {cc}: " + "  ".join(f"{k_} {v[0]:.0f}/{v[1]:.0f}" for k_, v in row.items()))
     if steps:
         print(f"step (top to next top, slowest wave) median {np.median(steps):.0f} ticks")
+    # per wave (chunk 1): median over workgroups of its stage-1 length, its stage-1 end after the
+    # step top of the workgroup's earliest wave, and how often it is the workgroup's slowest
+    t = st[:, :, 8: 16]
+    top = t[:, :, 0].min(1, keepdims=True)
+    s1 = t[:, :, 4] - t[:, :, 3]
+    end = t[:, :, 4] - top
+    slow = np.bincount(s1.argmax(1), minlength=8) / s1.shape[0]
+    for w in range(8):
+        print(f"   wave {w}: stage1 {np.median(s1[:, w]):.0f}  stage1 end {np.median(end[:, w]):.0f}  "
+              f"stage2 {np.median(t[:, w, 6] - t[:, w, 5]):.0f}  slowest in {100 * slow[w]:.0f} % of workgroups")
 
 
 if __name__ == "__main__":
