@@ -33,11 +33,6 @@
 namespace bcfft {
 
 namespace dm64g {
-// wave priority falling through stage 1 (1) and stage 2 (2): set_prio
-#ifndef BCFFT_DM64G_PRIO
-#define BCFFT_DM64G_PRIO 0
-#endif
-constexpr int PRIO = BCFFT_DM64G_PRIO;
 using namespace dmh;
 
 constexpr int B = 64, NI = 64, KS = 4, NOG = 32, TT = 8, NW = 8;
@@ -155,7 +150,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64g_kernel(
     for (int pr = 0; pr < 2; ++pr) xwb[pr] = 256 * g + 64 * (pr ^ (g & 1)) + 4 * b16;
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
-      if constexpr ((PRIO & 1) != 0) set_prio(3 - h);
       float xq[2][8];
       const char* rowp = slot + (16 * h + b16) * (B * ES);
 #pragma unroll
@@ -273,7 +267,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64g_kernel(
     uint32_t yh[BW][NT][2];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      if constexpr ((PRIO & 2) != 0) set_prio(3 - p);
       Breg& br = breg[p & 1];
       const __amdgpu_buffer_rsrc_t brs = b_rsrc(g);
       const int vo = opaque(lane) * 16;

@@ -46,11 +46,6 @@ constexpr int ABL = BCFFT_DMG_ABL;
 #else
 constexpr int ABL = 0;
 #endif
-// wave priority falling through stage 1 (1), stage 2 (2) and stage 3 (4): set_prio
-#ifndef BCFFT_DMG_PRIO
-#define BCFFT_DMG_PRIO 0
-#endif
-constexpr int PRIO = BCFFT_DMG_PRIO;
 
 constexpr int B = 128, NI = 32, KS = 2, NOG = 32, TT = 8, NW = 8;
 constexpr int BW = 8, NT = 2;                       // bins per wave, 16-wide N-tiles per group
@@ -212,7 +207,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmg_kernel(
 #endif
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      if constexpr ((PRIO & 1) != 0) set_prio(2 - h);
 #ifdef BCFFT_S1_ILP
       float xv8[2][2][8];
 #pragma unroll
@@ -356,7 +350,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmg_kernel(
     uint32_t yh[BW][NT][2];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      if constexpr ((PRIO & 2) != 0) set_prio(3 - p);
       Breg& br = breg[p & 1];
       const __amdgpu_buffer_rsrc_t brs = b_rsrc(g);
       const int vo = opaque(lane) * 16;
@@ -437,7 +430,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmg_kernel(
     }
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      if constexpr ((PRIO & 4) != 0) set_prio(3 - mt);
       f32x4 E[NT], O[NT];
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
