@@ -46,6 +46,12 @@
 namespace bcfft {
 
 namespace dmm {
+// wave priority falling through gate/up stage 2 (1), down stage 2 (2), gate/up stage 3 and
+// down stage 1 (4): set_prio
+#ifndef BCFFT_DMM_PRIO
+#define BCFFT_DMM_PRIO 7
+#endif
+constexpr int PRIO = BCFFT_DMM_PRIO;
 using namespace dmh;
 constexpr int B = 128, NI = 32, KS = 2, NOG = 32, TT = 8, NW = 8;
 constexpr int BW = 8, NT = 2;                       // bins per wave, 16-wide N-tiles
@@ -297,6 +303,7 @@ __global__ __launch_bounds__(512, 2) void bc_mlp_dmm_kernel(
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int fb = 0; fb < BW; ++fb) {
+        if constexpr ((PRIO & 1) != 0) set_prio(3 - 4 * (ks * BW + fb) / (KS * BW));
         uint4 raw = *reinterpret_cast<const uint4*>(ab + 4096 * ks + 64 * (fb ^ ((fb >> 2) & 1)));
         if (wave == 0 && fb == 0) {
           raw.x = pkmul(raw.x, gmul0[ks]); raw.y = pkmul(raw.y, gmul0[ks]);
@@ -340,6 +347,7 @@ __global__ __launch_bounds__(512, 2) void bc_mlp_dmm_kernel(
   // 4 KiB as bcfft_dmk.hip's x chunk: element e of block row r in unit e >> 3, stored at unit
   // (e >> 3) ^ r. Rows past n_h are zero (the two-launch path's DMA reads zeros there).
   auto gu_stage3 = [&](int g) {
+    if constexpr ((PRIO & 4) != 0) set_prio(3);
     const int l = opaque(lane);
     const int o16 = l & 15, gq = l >> 4;
     char* slot = wr + wave * SLOT;
@@ -411,6 +419,7 @@ __global__ __launch_bounds__(512, 2) void bc_mlp_dmm_kernel(
   // ---- down stage 1 (wave w, WR slot w): the h chunk -> X units in place (bcfft_dmk.hip's
   // stage 1: per-(token, chunk) exponent with HEAD headroom)
   auto dn_stage1 = [&]() {
+    if constexpr ((PRIO & 4) != 0) set_prio(1);
     const int l = opaque(lane);
     const int b16 = l & 15, g = l >> 4;
     const int q4 = (l & 15) >> 2, p4 = l & 3;
@@ -530,6 +539,7 @@ __global__ __launch_bounds__(512, 2) void bc_mlp_dmm_kernel(
     const int vo = opaque(lane) * 16;
 #pragma unroll
     for (int fb = 0; fb < BW; ++fb) {
+      if constexpr ((PRIO & 2) != 0) set_prio(3 - 4 * fb / BW);
       uint4 raw = *reinterpret_cast<const uint4*>(ab + 64 * (fb ^ ((fb >> 2) & 1)));
       if (wave == 0 && fb == 0) {
         raw.x = pkmul(raw.x, amul0); raw.y = pkmul(raw.y, amul0);
