@@ -613,6 +613,14 @@ inline int64_t sn_workgroups(int64_t n_tokens, int n_out) { return (n_tokens + 3
 inline bool sn_pays(int64_t n_tokens, int n_out) {
   return n_tokens > 0 && sn_workgroups(n_tokens, n_out) <= device_cu_count();
 }
+// 2-token tiles (launch_forward_sn) while their workgroups also fit one round; BCFFT_SN_TT2=0
+// builds the 4-token tiles only
+#ifndef BCFFT_SN_TT2
+#define BCFFT_SN_TT2 1
+#endif
+inline bool sn_tt2(int64_t n_tokens, int n_out) {
+  return BCFFT_SN_TT2 != 0 && n_tokens > 0 && (n_tokens + 1) / 2 * ((n_out + 15) / 16) <= device_cu_count();
+}
 // DFT-on-MFMA kernel (bcfft_dm.hip): the STAT image's geometry subset b = 128, K = 4096
 bool dm_eligible(int n_in, int b);
 bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, int mode, const void* x, int64_t n, int n_out,

@@ -65,9 +65,8 @@ struct Geo {
   static_assert(PT * TT % NW == 0, "whole DMA pieces per wave");
   static constexpr int NFRAG = BW * KS;            // 16-B weight fragment loads per lane
   static_assert(NFRAG < 64, "vmcnt range");
-  static constexpr int UPW1 = TT * KS / NW;        // stage-1 units per wave
-  static constexpr int UPW3 = TT * MT / NW;        // stage-3 units per wave
-  static_assert(UPW1 * NW == TT * KS && UPW3 * NW == TT * MT, "whole units per wave");
+  static constexpr int UPW1 = (TT * KS + NW - 1) / NW;   // stage-1 units per wave (TT = 2: some waves idle)
+  static constexpr int UPW3 = (TT * MT + NW - 1) / NW;   // stage-3 units per wave
 };
 }  // namespace sn
 
@@ -164,6 +163,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_sn_kernel(
 #pragma unroll
   for (int iu = 0; iu < G::UPW1; ++iu) {
     const int u = wave + NW * iu;
+    if (u >= TT * KS) break;                        // wave-uniform
     const int tk = u / KS, c = u % KS;
     const int l = opaque(lane);
     const int b16 = l & 15, g = l >> 4;
@@ -342,6 +342,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_sn_kernel(
 #pragma unroll
   for (int iu = 0; iu < G::UPW3; ++iu) {
     const int u = wave + NW * iu;
+    if (u >= TT * MT) break;                        // wave-uniform
     const int tk = u / MT, mt = u % MT;
     const int l = opaque(lane);
     const int o16 = l & 15, g = l >> 4;
@@ -430,8 +431,16 @@ bool sn_eligible(int n_in, int b) { return stat_eligible(n_in, b); }
 bool launch_forward_sn(int b, int n_in, int xdt, bool yf32, const void* x, int64_t n, int n_out, const void* spec,
                        const void* bias, int bias_dt, void* y, hipStream_t s) {
   if (!sn_eligible(n_in, b)) return false;
-  if (b == 128) return launch_sn_dt<128, 2, 4>(xdt, yf32, x, n, n_out, spec, bias, bias_dt, y, s);
-  if (n_in == 64) return launch_sn_dt<64, 4, 4>(xdt, yf32, x, n, n_out, spec, bias, bias_dt, y, s);
-  return launch_sn_dt<64, 2, 4>(xdt, yf32, x, n, n_out, spec, bias, bias_dt, y, s);
+  // 2-token tiles where they still fit one round of workgroups: twice the workgroups, each with
+  // half the x and half the stage-1 / stage-3 work (the weight fragments per workgroup are the same)
+  const bool t2 = sn_tt2(n, n_out);
+  if (b == 128)
+    return t2 ? launch_sn_dt<128, 2, 2>(xdt, yf32, x, n, n_out, spec, bias, bias_dt, y, s)
+              : launch_sn_dt<128, 2, 4>(xdt, yf32, x, n, n_out, spec, bias, bias_dt, y, s);
+  if (n_in == 64)
+    return t2 ? launch_sn_dt<64, 4, 2>(xdt, yf32, x, n, n_out, spec, bias, bias_dt, y, s)
+              : launch_sn_dt<64, 4, 4>(xdt, yf32, x, n, n_out, spec, bias, bias_dt, y, s);
+  return t2 ? launch_sn_dt<64, 2, 2>(xdt, yf32, x, n, n_out, spec, bias, bias_dt, y, s)
+            : launch_sn_dt<64, 2, 4>(xdt, yf32, x, n, n_out, spec, bias, bias_dt, y, s);
 }
 }  // namespace bcfft

@@ -3,7 +3,8 @@
 exact=True: the same table, splits and scales; only the work split differs).
 
 The kernel serves the STAT geometries (b = 128 with K = 4096; b = 64 with K = 2048 or 4096), every
-x dtype and bias, one workgroup per 4-token tile and 16 output blocks; AUTO takes it up to
+x dtype and bias, one workgroup per 2- or 4-token tile (2 while those workgroups fit one round)
+and 16 output blocks; AUTO takes it up to
 BCFFT_SN_MAX_TOKENS tokens (BASELINE config 1: 4096 -> 4096, b = 64, N = 128, fp32). Tolerances as
 dftx: < 6e-4 relative Frobenius and < 1e-3 per token (north star) for fp32 outputs, ~1 ulp of the
 output rounding for 16-bit ones."""
@@ -41,7 +42,11 @@ CASES = [
     (4096, 11008, 128, 13, "bfloat16", "bfloat16", False),  # 86 output blocks: 6 N-tiles, last partial
     (4096, 4096, 128, 64, "float16", "float16", True),
     (4096, 4096, 128, 50, "bfloat16", "float32", True),     # promotion -> fp32 output
-    (4096, 4096, 128, 255, "float32", "float32", False),    # 64 tiles, the last one of 3 tokens
+    (4096, 4096, 128, 255, "float32", "float32", False),    # 128 2-token tiles, the last one of 1 token
+    # 4-token tiles (the 2-token grid would exceed one round of 256 workgroups)
+    (4096, 4096, 128, 400, "float32", "float32", True),
+    (4096, 4096, 64, 203, "bfloat16", "bfloat16", False),   # the last tile of 3 tokens
+    (2048, 3072, 64, 300, "float32", "float32", True),
 ]
 
 
@@ -112,3 +117,19 @@ def test_auto_takes_short_at_small_n(dev, b, n):
     ya = ops.forward(x, spec, None, b, 4096, algo="auto")
     ys = ops.forward(x, spec, None, b, 4096, algo="short")
     assert torch.equal(ya, ys)
+
+
+@pytest.mark.parametrize("b,k,n_small,n_big", [(64, 4096, 128, 130), (128, 4096, 256, 258), (64, 2048, 170, 172)])
+def test_tile_size_does_not_change_results(dev, b, k, n_small, n_big):
+    """The 2-token tiles (n_small fits one round of their workgroups) and the 4-token tiles
+    (n_big does not) give bit-identical rows: a token's stage 1, its MFMA rows in stage 2 and its
+    stage 3 do not depend on which tokens share its workgroup."""
+    from bcfft import ops
+    m = 3072 if k == 2048 else 4096
+    rng = np.random.default_rng(b + n_big)
+    c = torch.from_numpy((rng.standard_normal((m // b, k // b, b)) * 0.01).astype(np.float32)).to(dev)
+    x = torch.from_numpy(rng.standard_normal((n_big, k)).astype(np.float32)).to(dev)
+    spec = ops.spectra(c)
+    y_big = ops.forward(x, spec, None, b, m, algo="short")
+    y_small = ops.forward(x[:n_small].contiguous(), spec, None, b, m, algo="short")
+    assert torch.equal(y_small, y_big[:n_small])
