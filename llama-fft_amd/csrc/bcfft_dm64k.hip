@@ -222,6 +222,17 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) xwb[pr] = 256 * g + 64 * (pr ^ (g & 1)) + 4 * b16;
     if constexpr ((PRIO & 1) != 0) __builtin_amdgcn_s_setprio(2);
+    // the table fragments read once for both tokens (the DMA's memory clobber kept the compiler
+    // from hoisting them): 16 of the 20 1-KiB LDS reads per token were these (116.2 vs 117.6 us,
+    // profiles/r05rr_ab_dm64k_table_once.log)
+    bf16x8 tab[2][2][2];
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm)
+          tab[pr][mt][tm] = *reinterpret_cast<const bf16x8*>(lds + TB_OFF + 2048 * (2 * pr + mt) + 1024 * tm + 16 * l);
 #pragma unroll 1
     for (int t2 = 0; t2 < 2; ++t2) {
       const int tl = wave + 8 * t2;
@@ -244,8 +255,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
         for (int pr = 0; pr < 2; ++pr)
 #pragma unroll
           for (int mt = 0; mt < 2; ++mt) {
-            const char* tb = lds + TB_OFF + 2048 * (2 * pr + mt) + 16 * l;
-            const bf16x8 th = *reinterpret_cast<const bf16x8*>(tb), tlo = *reinterpret_cast<const bf16x8*>(tb + 1024);
+            const bf16x8 th = tab[pr][mt][0], tlo = tab[pr][mt][1];
             f32x4 a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(th, b0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
             a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tlo, b0, a, 0, 0, 0);
             a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(th, pr ? b1n : b1, a, 0, 0, 0);
