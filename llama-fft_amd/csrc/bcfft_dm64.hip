@@ -17,6 +17,9 @@
 #include "bcfft_device.h"
 #include "bcfft_dm_table.h"
 #include "bcfft_dm_common.h"
+#ifndef BCFFT_DM64_TAB_ONCE
+#define BCFFT_DM64_TAB_ONCE 1
+#endif
 
 namespace bcfft {
 
@@ -134,6 +137,22 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64_kernel(
     int xwb[2];
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) xwb[pr] = 256 * g + 64 * (pr ^ (g & 1)) + 4 * b16;
+#if BCFFT_DM64_TAB_ONCE
+    // A = F^T (16 bin-reals x 32 t) fragments, read once for the four quarters (the X stores
+    // between quarters kept the compiler from reusing them: 32 -> 8 transposed reads per token)
+    f16x8 afr[2][2];
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int c = 4 * pr + 2 * mt;
+        const s16x4 ra = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(lds + trb0 + 16 * (c ^ cx0)));
+        const s16x4 rb = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(lds + trb1 + 16 * (c ^ cx1)));
+        afr[pr][mt] = __builtin_bit_cast(f16x8, __builtin_shufflevector(ra, rb, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#endif
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
       // x of block 16h + b16: t = 8 g + j (unit g) and t + 32 (unit g + 4), j < 8
@@ -175,12 +194,16 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64_kernel(
       for (int pr = 0; pr < 2; ++pr)
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
+#if BCFFT_DM64_TAB_ONCE
+          const f16x8 af = afr[pr][mt];
+#else
           const int c = 4 * pr + 2 * mt;            // A = F^T (16 bin-reals x 32 t)
           const s16x4 ra = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
               (__attribute__((address_space(3))) s16x4*)(lds + trb0 + 16 * (c ^ cx0)));
           const s16x4 rb = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
               (__attribute__((address_space(3))) s16x4*)(lds + trb1 + 16 * (c ^ cx1)));
           const f16x8 af = __builtin_bit_cast(f16x8, __builtin_shufflevector(ra, rb, 0, 1, 2, 3, 4, 5, 6, 7));
+#endif
           acc[2 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, pr ? bdh : bah, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         }
       char* xb = slot + 2048 * h;
