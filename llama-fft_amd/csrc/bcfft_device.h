@@ -601,7 +601,7 @@ bool launch_forward_glu(int b, int n_in, int xdt, const void* x, int64_t n, int 
 void launch_stat_image(int b, int n_out, int n_in, void* spec, hipStream_t s);
 // the precise engine's e4m3 weight residual image (b = 128, K = 4096; after launch_stat_image)
 void launch_lo8_image(int n_out, void* spec, hipStream_t s);
-// short-N DFT kernel (bcfft_sn.hip): the STAT image's geometries, one workgroup per 4-token tile
+// short-N DFT kernel (bcfft_sn.hip): the STAT image's geometries, one workgroup per 4-token tile (2-token where those fit: sn_tt2)
 // and 16-wide N-tile, one workgroup per CU (LDS). AUTO takes it while those workgroups fit one
 // round on the device (sn_pays): measured against the persistent engines (tools/time_algos.py
 // --short, profiles/r05e_time_short.log) it wins through one round and loses from two (e.g.
