@@ -33,6 +33,11 @@ namespace bcfft {
 namespace sn {
 using namespace dmh;
 constexpr int NW = 8;
+// wave priority falling through stage 2's bins (set_prio; bcfft_dm64k.hip's finding)
+#ifndef BCFFT_SN_PRIO
+#define BCFFT_SN_PRIO 0
+#endif
+constexpr bool SN_PRIO = BCFFT_SN_PRIO != 0;
 
 template <int B, int KS, int TT, int ES>
 struct Geo {
@@ -299,9 +304,13 @@ __global__ __launch_bounds__(512, 2) void bc_forward_sn_kernel(
     const char* ab = lds + G::XI_OFF + at * G::TSX + a_prec * 64 + 16 * kb;
     const int yt = ml >> 4, o16 = ml & 15;
     char* yb = lds + G::XS_OFF + yt * G::TSY + 16 * o16;
+    // the Y stores after the bin loop: a store between two bins kept the compiler from issuing
+    // the next bin's A reads early (their LDS latency then sat on each bin's chain)
+    uint32_t yhs[BW], yls[BW];
 #pragma unroll
     for (int fb = 0; fb < BW; ++fb) {
       const int f = wave * BW + fb;
+      if constexpr (SN_PRIO) set_prio(3 - 4 * fb / BW);
       uint4 raw[KS];
 #pragma unroll
       for (int c = 0; c < KS; ++c) raw[c] = *reinterpret_cast<const uint4*>(ab + (c * H + f) * 128);
@@ -321,14 +330,18 @@ __global__ __launch_bounds__(512, 2) void bc_forward_sn_kernel(
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, rw), creg[fb][c], acc, 0, 0, 0);
       }
       constexpr float YS = 1.f / 2097152.f;          // 2^-21: |Y| < 2^14 in fp16
-      uint32_t yh, yl;                               // rows 4 yt + {re hi, re lo, im hi, im lo}
-      split2((acc[0] + acc[1]) * YS, (acc[2] + acc[3]) * YS, yh, yl);
-      if (yt < TT) {                                 // Y unit (prec, parity, 4-bin group, o) + 4 B per bin
+      // rows 4 yt + {re hi, re lo, im hi, im lo}
+      split2((acc[0] + acc[1]) * YS, (acc[2] + acc[3]) * YS, yhs[fb], yls[fb]);
+    }
+    if (yt < TT) {                                   // Y unit (prec, parity, 4-bin group, o) + 4 B per bin
+#pragma unroll
+      for (int fb = 0; fb < BW; ++fb) {
+        const int f = wave * BW + fb;
         const int j = f >> 1, pr = f & 1;
         char* w0 = yb + (((0 * 2 + pr) * G::JG + (j >> 2)) * 16) * 16 + 4 * (j & 3);
         char* w1 = yb + (((1 * 2 + pr) * G::JG + (j >> 2)) * 16) * 16 + 4 * (j & 3);
-        *reinterpret_cast<uint32_t*>(w0) = yh;
-        *reinterpret_cast<uint32_t*>(w1) = yl;
+        *reinterpret_cast<uint32_t*>(w0) = yhs[fb];
+        *reinterpret_cast<uint32_t*>(w1) = yls[fb];
       }
     }
   }
