@@ -92,18 +92,22 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmg_kernel(
   const int64_t n_mtiles = (n_tokens + TT - 1) / TT;
   const int64_t gstride = gridDim.x;
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+#ifdef BCFFT_STAMPS
+  ANALYSIS_INIT;
+  (void)ablate_flags_;
+#endif
   const uint4* bimg = reinterpret_cast<const uint4*>(stat + 4);
 
   // ---- x of token `wave` of M-tile m -> its slot by LDS-DMA (bcfft_dm8.hip's: the buffer range
   // zero-fills tokens past n_tokens; the slot's unit swizzle is applied to the source offsets)
-  auto dma_token = [&](int64_t m, char* region) {
+  auto dma_token = [&](int64_t m, char* region, int sl) {   // token slot sl of tile m
     if constexpr ((ABL & 16) != 0) return;
-    const int64_t tok = m * TT + wave;
+    const int64_t tok = m * TT + sl;
     const bool ok = tok < n_tokens;
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<char*>((const char*)xv) + (ok ? tok : 0) * K * ES, 0, ok ? K * ES : 0, 0x00020000);
     const int dl = opaque(lane);
-    const uint32_t dst0 = lds_base + (uint32_t)(region - lds) + wave * SLOT;
+    const uint32_t dst0 = lds_base + (uint32_t)(region - lds) + sl * SLOT;
     int vb[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -143,7 +147,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmg_kernel(
   // first group's first B pass
   Breg breg[2];
   const int64_t m0 = blockIdx.x;
-  dma_token(m0, lds);
+  dma_token(m0, lds, wave);
   {
     const uint4* tab = reinterpret_cast<const uint4*>(kDmF);
 #pragma unroll
@@ -524,31 +528,46 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmg_kernel(
   // m + stride is complete after group 0's pass 1 of tile m, at the latest.
   constexpr int NST = GLU ? 4 : 8;                  // y stores per wave and group
   int it = 0;
+  // stamps build (tools/timeline_dmg.py): slots of the workgroup's second tile, 0 top | 1 DMA
+  // issued | 2 stage 1 | 3 Ba | 4 A fragments | 5 Bx | per group g < 4: 6 + 4g stage 2 | 7 + 4g
+  // Bb | 8 + 4g stage 3 | 9 + 4g Bc
+#define DGS(o) do { if (it == 1) STAMP(o); } while (0)
   for (int64_t m = m0; m < n_mtiles; m += gstride, ++it) {
     char* region = lds + (it & 1) * REGION;
     char* other = lds + ((it + 1) & 1) * REGION;
     const int par = it & 1;
     const bool dma = m + gstride < n_mtiles;
-    if (dma) dma_token(m + gstride, other);         // R' was released by the previous tile's Bc
+    DGS(0);
+    if (dma) dma_token(m + gstride, other, wave);   // R' was released by the previous tile's Bc
+    DGS(1);
     stage1(region, par);
+    DGS(2);
     lds_barrier();                                  // Ba: X units and scales complete
+    DGS(3);
     load_a(region, par);
     load_pass(0, 1, breg[1]);
+    DGS(4);
     lds_barrier();                                  // Bx: every wave holds its A fragments
+    DGS(5);
     for (int g = 0; g < n_groups; ++g) {
       // group 0: [pass 0, (previous group's stores), (x DMA), pass 1]; later groups: [pass 0,
       // pass 1, previous group's stores]
       stage2(region, g);
+      if (g < 4) DGS(6 + 4 * g);
       lds_barrier();                                // Bb: Y units complete
+      if (g < 4) DGS(7 + 4 * g);
       const bool more = g + 1 < n_groups;
       if (more) load_pass(g + 1, 0, breg[0]);
       else if (dma) load_pass(0, 0, breg[0]);       // the next tile's group 0 (consumed there)
       stage3(region, par, m, g, [&] {
         if (more) load_pass(g + 1, 1, breg[1]);
       });
+      if (g < 4) DGS(8 + 4 * g);
       lds_barrier();                                // Bc: staging reads done (slots reusable)
+      if (g < 4) DGS(9 + 4 * g);
     }
   }
+#undef DGS
 }
 
 }  // namespace bcfft
@@ -584,3 +603,10 @@ void launch_forward_dmg(const void* x, int64_t n, int n_out, const void* spec, c
   else launch_dmg<false, false>(x, n, n_out, spec, bias, bias_dt, y, s);
 }
 }  // namespace bcfft
+
+#ifdef BCFFT_STAMPS
+extern "C" int bcfft_set_stamps_dmg(void* buf) {
+  unsigned long long* p = (unsigned long long*)buf;
+  return hipMemcpyToSymbol(HIP_SYMBOL(bcfft::g_stamps), &p, sizeof(p)) == hipSuccess ? 0 : BCFFT_ERR_HIP;
+}
+#endif
