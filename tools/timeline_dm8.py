@@ -52,6 +52,12 @@ def main():
             d = st[:, :, cur] - st[:, :, prev]
             print(f"  {NAMES[i]:22s} slowest {np.median(d.max(1)):7.0f}  fastest {np.median(d.min(1)):7.0f}")
             prev = cur
+    # per wave, iteration 3 (steady state): median phase lengths over workgroups
+    base = 1 + 6 * 3
+    if (st[:, :, base: base + 6] != 0).all():
+        d = np.diff(st[:, :, base: base + 6], axis=2)
+        for w in range(8):
+            print(f"   wave {w}: " + "  ".join(f"{NAMES[i + 1]} {np.median(d[:, w, i]):.0f}" for i in range(5)))
 
 
 if __name__ == "__main__":
