@@ -415,6 +415,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64_kernel(
 #ifndef BCFFT_DM64_MIX
 #define BCFFT_DM64_MIX 1
 #endif
+#ifndef BCFFT_DM64_YPRIO
+#define BCFFT_DM64_YPRIO 1
+#endif
     // waves 0-3 run stage 3 and the next tile's x DMA before their stage 1 (bcfft_dm8.hip's mixed
     // order: a memory-heavy and a transform-heavy wave per SIMD, two DMA bursts per phase)
     if (BCFFT_DM64_MIX && wave < 4 && it > 0 && have) {
@@ -431,7 +434,12 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64_kernel(
     } else {
       if (have) {
         wait_vmcnt<0>();                            // this wave's x (and its older y stores)
+        // YPRIO: the transform-first (younger) waves issue ahead of their partner's stage 3
+        // (bcfft_dm8.hip's finding): 50.3 -> 47.9 us over six interleaved passes
+        // (profiles/r05ac_ab_dm64_yprio.log)
+        if (BCFFT_DM64_YPRIO && BCFFT_DM64_MIX) __builtin_amdgcn_s_setprio(BCFFT_DM64_YPRIO);
         stage1(region, par);
+        if (BCFFT_DM64_YPRIO && BCFFT_DM64_MIX) __builtin_amdgcn_s_setprio(0);
       }
       if (it > 0) stage3(other, par ^ 1, m - gstride);
       if (m + gstride < n_mtiles) {

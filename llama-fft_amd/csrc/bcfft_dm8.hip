@@ -548,7 +548,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
 #define BCFFT_DM8_MIX 1
 #endif
 #ifndef BCFFT_DM8_YPRIO
-#define BCFFT_DM8_YPRIO 0
+#define BCFFT_DM8_YPRIO 1
 #endif
     // waves 0-3 run stage 3 and the next tile's x DMA before their stage 1, waves 4-7 after it:
     // each SIMD then pairs a memory-heavy wave with a transform-heavy one, and the 64 DMA pieces
@@ -573,7 +573,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
 #else
         STAMP(sb + 1);
         // YPRIO: the transform-first waves (the younger of each SIMD pair) issue ahead of their
-        // partner's stage 3 (their stage 1 was the tile's critical path, profiles/r05f4_timeline_dm8.txt)
+        // partner's stage 3: their stage 1 was the tile's critical path (6.1 k cycles against 2.6 k,
+        // profiles/r05f4_timeline_dm8.txt); with it both waves finish at ~8.1 k and the kernel
+        // reads 36.3 -> 35.9 us (profiles/r05ab_ab_dm8_yprio.log)
         if (BCFFT_DM8_YPRIO && BCFFT_DM8_MIX) __builtin_amdgcn_s_setprio(BCFFT_DM8_YPRIO);
         stage1(region, par, wave, true, std::integral_constant<int, 0>{});   // waits per half for this wave's x (and its older y stores)
         if (BCFFT_DM8_YPRIO && BCFFT_DM8_MIX) __builtin_amdgcn_s_setprio(0);
