@@ -466,21 +466,47 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256_kernel(
     char* other = lds + ((it + 1) & 1) * REGION;
     const int par = it & 1;
     const bool have = m < n_mtiles;
-    if (it > 0) stage3(other, par ^ 1, m - gstride);
     const bool pf = m + gstride < n_mtiles;
-    if (pf) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
-      dma_token(m + gstride, other);
-    }
-    if (!have) break;
-    if (pf) {
-      if (it > 0) wait_vmcnt<8 + NDMA>();
-      else wait_vmcnt<NDMA>();
+#ifndef BCFFT_DM256_MIX
+#define BCFFT_DM256_MIX 1
+#endif
+#ifndef BCFFT_DM256_YPRIO
+#define BCFFT_DM256_YPRIO 1
+#endif
+    if (!BCFFT_DM256_MIX || (wave < 4 && it > 0 && have)) {
+      // stage 3 of the previous tile, the next tile's x DMA, then stage 1 (with MIX: waves 0-3)
+      if (it > 0) stage3(other, par ^ 1, m - gstride);
+      if (pf) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
+        dma_token(m + gstride, other);
+      }
+      if (!have) break;
+      if (pf) {
+        if (it > 0) wait_vmcnt<8 + NDMA>();
+        else wait_vmcnt<NDMA>();
+      } else {
+        if (it > 0) wait_vmcnt<8>();
+        else wait_vmcnt<0>();
+      }
+      stage1(region, par);
     } else {
-      if (it > 0) wait_vmcnt<8>();
-      else wait_vmcnt<0>();
+      // MIX (waves 4-7, and every wave of the first and last iterations): stage 1 first, at a
+      // higher priority than the partner wave's stage 3 (bcfft_dm8.hip's mixed order and YPRIO):
+      // 39.2 -> 36.8 us over six interleaved passes, the order alone 38.7
+      // (profiles/r05ad_ab_dm256_mix_yprio.log)
+      if (have) {
+        wait_vmcnt<0>();                            // this wave's x (issued an iteration ago)
+        if (BCFFT_DM256_YPRIO) __builtin_amdgcn_s_setprio(BCFFT_DM256_YPRIO);
+        stage1(region, par);
+        if (BCFFT_DM256_YPRIO) __builtin_amdgcn_s_setprio(0);
+      }
+      if (it > 0) stage3(other, par ^ 1, m - gstride);
+      if (pf) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
+        dma_token(m + gstride, other);
+      }
+      if (!have) break;
     }
-    stage1(region, par);
     lds_barrier();                                  // Ba: X units and scales complete
     stage2(region, par);
     lds_barrier();                                  // Bb: Y units complete
