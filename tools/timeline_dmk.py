@@ -57,6 +57,13 @@ def main():
             d = st[:, :, cur] - st[:, :, prev]
             print(f"  {NAMES.get(i, i):24s} slowest {np.median(d.max(1)):7.0f}  fastest {np.median(d.min(1)):7.0f}")
             prev = cur
+    # per wave, tile 1, chunk step 2 (steady state): median over workgroups
+    base = 1 + 30
+    cols = [(10, 9), (11, 10), (12, 11)]          # (end slot, start slot) of c2's three phases
+    if all((st[:, :, base + a] != 0).all() and (st[:, :, base + b] != 0).all() for a, b in cols):
+        for w in range(8):
+            parts = [f"{NAMES[a]} {np.median(st[:, w, base + a] - st[:, w, base + b]):.0f}" for a, b in cols]
+            print(f"   wave {w}: " + "  ".join(parts))
 
 
 if __name__ == "__main__":
