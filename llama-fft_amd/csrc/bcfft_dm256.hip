@@ -613,7 +613,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256k_kernel(
   auto wait_b = [&](auto n_tag, u32x4 (&breg)[BPW]) {
     constexpr int N = decltype(n_tag)::value;
     static_assert(N >= 0 && N < 64, "vmcnt");
-    asm volatile("s_waitcnt vmcnt(%16)"
+    asm volatile("s_waitcnt vmcnt(%16) ; bcfft-wait %0 %1 %2 %3 %4 %5 %6 %7 %8 %9 %10 %11 %12 %13 %14 %15"
                  : "+v"(breg[0]), "+v"(breg[1]), "+v"(breg[2]), "+v"(breg[3]), "+v"(breg[4]), "+v"(breg[5]),
                    "+v"(breg[6]), "+v"(breg[7]), "+v"(breg[8]), "+v"(breg[9]), "+v"(breg[10]), "+v"(breg[11]),
                    "+v"(breg[12]), "+v"(breg[13]), "+v"(breg[14]), "+v"(breg[15])

@@ -177,7 +177,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
   auto wait_b = [&](auto n_tag, u32x4 (&breg)[BW][KC][NT]) {
     constexpr int N = decltype(n_tag)::value;
     static_assert(N >= 0 && N < 64, "vmcnt");
-    asm volatile("s_waitcnt vmcnt(%16)"
+    asm volatile("s_waitcnt vmcnt(%16) ; bcfft-wait %0 %1 %2 %3 %4 %5 %6 %7 %8 %9 %10 %11 %12 %13 %14 %15"
                  : "+v"(breg[0][0][0]), "+v"(breg[0][0][1]), "+v"(breg[0][1][0]), "+v"(breg[0][1][1]),
                    "+v"(breg[1][0][0]), "+v"(breg[1][0][1]), "+v"(breg[1][1][0]), "+v"(breg[1][1][1]),
                    "+v"(breg[2][0][0]), "+v"(breg[2][0][1]), "+v"(breg[2][1][0]), "+v"(breg[2][1][1]),

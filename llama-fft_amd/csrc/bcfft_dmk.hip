@@ -201,7 +201,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
   auto wait_b = [&](auto n_tag, int nt, u32x4 (&breg)[BPW][NT]) {
     constexpr int N = decltype(n_tag)::value;
     static_assert(N >= 0 && N < 64, "vmcnt");
-    asm volatile("s_waitcnt vmcnt(%8)"
+    asm volatile("s_waitcnt vmcnt(%8) ; bcfft-wait %0 %1 %2 %3 %4 %5 %6 %7"
                  : "+v"(breg[0][nt]), "+v"(breg[1][nt]), "+v"(breg[2][nt]), "+v"(breg[3][nt]),
                    "+v"(breg[4][nt]), "+v"(breg[5][nt]), "+v"(breg[6][nt]), "+v"(breg[7][nt])
                  : "n"(N) : "memory");
@@ -630,9 +630,27 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
       char* region = lds + rsel * REGION;
       char* other = lds + (rsel ^ 1) * REGION;
       wait_vmcnt<16>();                             // x(c) (older than B(c))
+#ifdef BCFFT_DMK_LATE_DMA
+      // analysis build: the younger waves 4-7 issue this step's x DMA after
+      // their stage 1 instead of before it (round 5's failing variant, re-created)
+      const bool late = wave >= 4;
+      if (!late) {
+        if (c + 1 < c1) dma_chunk(m, c + 1, other);
+        else dma_chunk(m + gstride, c0, other);
+      }
+      stage1(region);
+      if (late) {
+        if (c + 1 < c1) dma_chunk(m, c + 1, other);
+        else dma_chunk(m + gstride, c0, other);
+#if BCFFT_DMK_LATE_DMA == 2
+        wait_vmcnt<0>();                            // bisection: the late DMA landed before Ba
+#endif
+      }
+#else
       if (c + 1 < c1) dma_chunk(m, c + 1, other);
       else dma_chunk(m + gstride, c0, other);       // zero-filled past the last tile
       stage1(region);
+#endif
       if (c <= 5) DSTAMP(7 + 3 * (c - 1));
       lds_barrier();                                // Ba
       if (c <= 5) DSTAMP(8 + 3 * (c - 1));

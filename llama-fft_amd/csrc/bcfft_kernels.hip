@@ -861,8 +861,11 @@ int bcfft_forward_ws(const void* x, int x_dtype, int64_t n_tokens, int in_featur
   float* ws = (workspace && need > 0 && workspace_bytes >= need) ? (float*)workspace : nullptr;
   hipStream_t s = (hipStream_t)stream;
   if (algo == BCFFT_ALGO_SHORT) {
-    bcfft::launch_forward_sn(block_size, n_in, x_dtype, y_dtype == BCFFT_F32, x, n_tokens, n_out, spectra, bias,
-                             bias_dtype, y, s);
+    // eligibility was checked by resolve_algo; a launcher that still declines (a future geometry or
+    // dtype rule out of step with it) must not report BCFFT_OK over an unwritten y
+    if (!bcfft::launch_forward_sn(block_size, n_in, x_dtype, y_dtype == BCFFT_F32, x, n_tokens, n_out, spectra, bias,
+                                  bias_dtype, y, s))
+      return refuse("bcfft_forward", algo, n_in, block_size, x_dtype, y_dtype);
     return record_launch();
   }
   if (algo == BCFFT_ALGO_DFT && dmk) {

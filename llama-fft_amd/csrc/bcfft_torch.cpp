@@ -101,19 +101,22 @@ at::Tensor forward_hip(const at::Tensor& x, const at::Tensor& spec, const std::o
   const int xc = dtype_code(xa.scalar_type()), yc = dtype_code(y.scalar_type());
   // split-K workspace (short grids of the MFMA and streamed-weight kernels) from torch's allocator;
   // the query is host logic keyed by the geometry, so a layer called again with the same shape
-  // (every decode step, every prefill batch of one size) reuses the last answer
+  // (every decode step, every prefill batch of one size) reuses the last answer. The answer depends
+  // on the current device's CU count (split-K slices, the short-N rule), so the device is part of
+  // the key: one thread driving GPUs of different sizes re-queries per device.
   struct WsKey {
     int64_t n, k, o, b, algo;
-    int xc, yc;
+    int xc, yc, dev;
     bool operator==(const WsKey& r) const {
-      return n == r.n && k == r.k && o == r.o && b == r.b && algo == r.algo && xc == r.xc && yc == r.yc;
+      return n == r.n && k == r.k && o == r.o && b == r.b && algo == r.algo && xc == r.xc && yc == r.yc &&
+             dev == r.dev;
     }
   };
-  thread_local WsKey ws_key{-1, 0, 0, 0, 0, 0, 0};
+  thread_local WsKey ws_key{-1, 0, 0, 0, 0, 0, 0, -1};
   thread_local int64_t ws_cached = 0;
   int64_t ws_bytes = 0;
   if (split_k) {
-    const WsKey key{n, k, out_features, block_size, algo, xc, yc};
+    const WsKey key{n, k, out_features, block_size, algo, xc, yc, (int)x.device().index()};
     if (!(key == ws_key)) {
       ws_cached = bcfft_forward_workspace_bytes_io(n, (int)k, (int)out_features, (int)block_size, (int)algo, xc, yc);
       ws_key = key;

@@ -26,6 +26,7 @@ from typing import Dict
 
 import torch
 import torch.nn as nn
+from torch.autograd.function import once_differentiable
 
 from bcfft import ops as _ops
 from bcfft import _lib
@@ -117,7 +118,11 @@ class _BCFunction(torch.autograd.Function):
         return y
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, dy):
+        # once_differentiable: the backward runs its kernels under no_grad on both host paths (the
+        # C++ operator and the ctypes call), so backward(create_graph=True) gives first-order
+        # gradients either way, and a second differentiation raises the same error on both
         x2d, c, bias = ctx.saved_tensors
         m = ctx.module
         dx = dc = dbias = None

@@ -53,18 +53,25 @@ def main():
     with torch.inference_mode():
         y = sharded_forward(layer, xd)                   # shard + RCCL all_gather_into_tensor
         # a second gather of another size; 600 tokens keep AUTO on the engine of the 1003-token
-        # call (up to 512 it takes the short-N kernel, whose roundings differ)
+        # call (bit-equal rows) ...
         y2 = gather_rows(layer(xd[:600]), 600)
+        # ... and a sub-threshold shard (500 tokens: AUTO takes the short-N kernel while its grid
+        # fits one round of CUs, whose roundings differ from dftx's): AUTO results are not
+        # batch-size invariant, so this gather is compared with the engines'
+        # mutual tolerance, not bit for bit
+        y3 = gather_rows(layer(xd[:500]), 500)
     torch.cuda.synchronize()
     ref = O.bc_forward(x, c, bv)
     g = y.cpu().numpy()
     err = float(np.linalg.norm(g - ref) / np.linalg.norm(ref))
     assert y.shape == (n, k) and err < 6e-4, err
     assert torch.equal(y2, y[:600])
+    d3 = float(torch.linalg.norm(y3 - y[:500]) / torch.linalg.norm(y[:500]))
+    assert y3.shape == (500, k) and d3 < 2e-5, d3
 
     r = bench.run_partitioned(layer, xd, n, 3, 1, 1, barrier, dev, settle_ms=0.0, allgather=True, repeats=2)
     assert r["gather_wall"] is not None and r["gather_wall"] > 0 and r["wall"] > 0, r
-    print("RCCL_OK " + json.dumps({"backend": dist.get_backend(), "rel_err": err, "world": dist.get_world_size(),
+    print("RCCL_OK " + json.dumps({"backend": dist.get_backend(), "rel_err": err, "sub_threshold_rel": d3, "world": dist.get_world_size(),
                                    "wall_ms": r["wall"], "gather_wall_ms": r["gather_wall"],
                                    "rccl_version": ".".join(map(str, torch.cuda.nccl.version()))
                                    if hasattr(torch.cuda, "nccl") else None}), flush=True)

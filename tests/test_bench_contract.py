@@ -35,7 +35,7 @@ def test_engine_resolution_mirrors_auto_rule(built_lib):
     assert bench.resolved_kernel("valu", 4096, 128)[1] == "bc_forward_valu_kernel"
     assert bench.resolved_kernel("auto", 4096, 128, "bf16", 11008, 8192)[1] == "bc_forward_dmg_kernel"
     # short token counts on the STAT geometries: the short-N kernel (bcfft_sn.hip), e.g. a decode step
-    # and BASELINE config 1; the persistent engines from BCFFT_SN_MAX_TOKENS + 1 tokens
+    # and BASELINE config 1; the persistent engines once the short grid exceeds the CUs (sn_pays)
     assert bench.resolved_kernel("auto", 4096, 128, "bf16", 11008, 20)[:2] == ("short", "bc_forward_sn_kernel")
     assert bench.resolved_kernel("auto", 4096, 64, "fp32", 4096, 128)[:2] == ("short", "bc_forward_sn_kernel")
     assert bench.resolved_kernel("auto", 4096, 128, "fp32", 4096, 1)[1] == "bc_forward_sn_kernel"

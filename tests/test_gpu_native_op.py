@@ -109,3 +109,23 @@ def test_operands_on_other_device_or_strided(dev, monkeypatch, native):
         with pytest.raises(ValueError, match="spectra is on cpu"):
             ops.forward_glu(x, sgu.cpu(), 128, 4096)
         assert torch.equal(ops.forward(x, spec, None, 128, 4096), ops.forward(x, spec, None, 128, 4096))
+
+
+@pytest.mark.parametrize("native", [True, False])
+def test_backward_create_graph_same_on_both_paths(dev, monkeypatch, native):
+    """backward(create_graph=True) through BlockCirculantLinear: first-order gradients equal to the
+    plain backward on the C++ operator path and the ctypes path alike (the custom Function's
+    backward is once_differentiable: its kernels run under no_grad), and differentiating them again
+    raises the same RuntimeError on both."""
+    from patch_llama_fft import BlockCirculantLinear
+    torch.manual_seed(3)
+    layer = BlockCirculantLinear(256, 128, block_size=64, bias=True).to(dev)
+    x = torch.randn(6, 256, device=dev, requires_grad=True)
+    with monkeypatch.context() as mp:
+        if not native:
+            _ctypes_path(mp)
+        gx, gc = torch.autograd.grad(layer(x).square().sum(), (x, layer.c))
+        gx2, gc2 = torch.autograd.grad(layer(x).square().sum(), (x, layer.c), create_graph=True)
+        assert torch.equal(gx, gx2.detach()) and torch.equal(gc, gc2.detach())
+        with pytest.raises(RuntimeError, match="once_differentiable|differentiate"):
+            torch.autograd.grad(gx2.sum(), x)

@@ -65,9 +65,12 @@ def build_model(args, dev):
     return model.eval()
 
 
+COLL_DEV = "cuda"        # where collective operands live: "cpu" under --backend gloo
+
+
 def sync_max(t: float) -> float:
     if dist.is_initialized():
-        v = torch.tensor([t], dtype=torch.float64, device="cuda")
+        v = torch.tensor([t], dtype=torch.float64, device=COLL_DEV)
         dist.all_reduce(v, op=dist.ReduceOp.MAX)
         return float(v.item())
     return t
@@ -217,6 +220,10 @@ def main(argv=None):
     ap.add_argument("--temperature", type=float, default=1.0)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--config-overrides", default="{}", help="JSON LlamaConfig overrides (tests)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group under a launcher: nccl (RCCL, one GPU per rank; the product path) "
+                         "or gloo (tests: several ranks sharing one GPU, which RCCL refuses; the logits "
+                         "gather then runs on host copies)")
     ap.add_argument("--dump-logits", default="",
                     help="rank 0 saves the student's last-token logits of ALL prompts (after the all-gather "
                          "when distributed) and the teacher's local ones to this .pt file (tests)")
@@ -233,11 +240,19 @@ def main(argv=None):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if not torch.cuda.is_available():
         raise SystemExit("model_bench needs a ROCm GPU (the BC engine has no CPU path)")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    global COLL_DEV
+    gloo = args.backend == "gloo"
+    # gloo: ranks may share a device (the one-GPU test of the world > 1 path)
+    dev_index = local % torch.cuda.device_count() if gloo else local
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     own_pg = launched and not dist.is_initialized()
     if own_pg:
-        dist.init_process_group("nccl", device_id=dev)
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+    COLL_DEV = "cpu" if gloo else "cuda"
 
     if args.prompts < world:
         raise SystemExit(f"--prompts {args.prompts} < {world} ranks: every rank needs a prompt")
@@ -247,7 +262,7 @@ def main(argv=None):
     mine = E.prompt_shard(prompts, world, rank)
     batches = [tuple(t.to(dev) for t in b) for b in E.iter_batches(mine, args.batch_size, cfg.pad_token_id)]
     my_tokens = sum(int(a.sum()) for _, a in mine)
-    tok = torch.tensor([my_tokens], device=dev)
+    tok = torch.tensor([my_tokens], device=COLL_DEV)
     if dist.is_initialized():
         dist.all_reduce(tok)
     total_tokens = int(tok.item())
@@ -289,7 +304,7 @@ def main(argv=None):
         if dist.is_initialized():
             barrier()
             tg = time.perf_counter()
-            all_last = gather_prompt_logits(student_last, args.prompts)
+            all_last = gather_prompt_logits(student_last.to(COLL_DEV), args.prompts).to(dev)
             barrier()
             res["allgather_logits_s"] = sync_max(time.perf_counter() - tg)
         if args.dump_logits and rank == 0 and bi == 0:

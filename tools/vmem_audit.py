@@ -1,0 +1,352 @@
+"""Static audit of the vector-memory (VMEM) ordering in the gfx950 code objects (CPU only).
+
+The streamed-weight kernels issue some loads from inline asm (`buffer_load_dwordx4 v[..] ...` for
+the B fragments, `buffer_load_dwordx4 ... lds` for the x DMA): the compiler does not count them in
+its s_waitcnt bookkeeping, and it believes an asm load's destination registers hold their value as
+soon as the asm statement ends. The program then relies on hand-placed `s_waitcnt vmcnt(N)`, and on
+the compiler never touching those registers (copy, spill, reuse) before the covering wait.
+
+This tool checks exactly that on the compiled ISA (`hipcc -S` output, per kernel):
+
+  * every VMEM instruction (buffer_/global_/flat_/scratch_, loads, stores, LDS DMA, atomics) is an
+    entry in an in-order queue; `s_waitcnt vmcnt(n)` retires all but the n youngest (gfx9: loads,
+    stores and LDS-DMA count together, in issue order; MI355X_MICROARCH.md);
+  * a dataflow over the kernel's control-flow graph keeps, per load still possibly in flight, the
+    MINIMUM number of younger VMEM instructions over all paths (a load is retired by vmcnt(n) only
+    if at least n younger ones were issued after it on every path): the conservative state;
+  * any instruction that names a VGPR / AGPR of a possibly-in-flight load's destination (reads it:
+    a stale value; writes it: the landing load overwrites the new value) is reported, with the load
+    that is still in flight and the path-minimum count of younger operations.
+
+Loads the compiler emitted itself are covered by its own waits (asm VMEM it cannot see only adds
+younger operations, which makes its waits stricter), so every report is about hand-counted waits
+or compiler register traffic around an asm load.
+
+usage: python tools/vmem_audit.py file.s [kernel-substring]      (exit 1 when a hazard is found)
+       python tools/vmem_audit.py --build [DEFS...]               (compile every product TU, audit all)
+"""
+import os
+import re
+import subprocess
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CAP = 64
+VMEM_RE = re.compile(r"^(buffer|global|flat|scratch)_")
+BRANCH_RE = re.compile(r"^s_(branch|cbranch_\w+)$")
+REG_RE = re.compile(r"\b([va])\[(\d+):(\d+)\]|\b([va])(\d+)\b")
+
+
+def regs_of(text):
+    out = set()
+    for m in REG_RE.finditer(text):
+        if m.group(1):
+            f, lo, hi = m.group(1), int(m.group(2)), int(m.group(3))
+            out.update((f, r) for r in range(lo, hi + 1))
+        else:
+            out.add((m.group(4), int(m.group(5))))
+    return out
+
+
+class Insn:
+    __slots__ = ("idx", "line", "op", "args", "asm", "vmem", "lds_dma", "is_load", "dest", "touch", "vmcnt", "target")
+
+    def __init__(self, idx, line, text, asm):
+        self.idx, self.line, self.asm = idx, line, asm
+        parts = text.split(None, 1)
+        self.op = parts[0]
+        self.args = parts[1] if len(parts) > 1 else ""
+        a = self.args.split(";")[0]
+        self.vmem = bool(VMEM_RE.match(self.op)) and not self.op.startswith(("buffer_wbl2", "buffer_inv"))
+        self.lds_dma = self.vmem and re.search(r"\blds\b", a) is not None
+        self.is_load = self.vmem and ("_load" in self.op or ("atomic" in self.op and re.search(r"\b(glc|sc0)\b", a)))
+        ops = [o.strip() for o in a.split(",")]
+        self.dest = regs_of(ops[0]) if (self.is_load and not self.lds_dma and ops) else set()
+        self.touch = regs_of(a)
+        self.vmcnt = None
+        self.target = None
+        if self.op == "s_waitcnt":
+            m = re.search(r"vmcnt\((\d+)\)", a)
+            if m:
+                self.vmcnt = int(m.group(1))
+            elif re.fullmatch(r"\s*0\s*", a):
+                self.vmcnt = 0
+
+
+def parse_functions(path):
+    """{kernel name: [lines of its body]} from a hipcc -S listing."""
+    funcs, cur, name = {}, None, None
+    for ln in open(path):
+        s = ln.rstrip("\n")
+        m = re.match(r"^(_Z\w+):", s)
+        if m:
+            name, cur = m.group(1), []
+            funcs[name] = cur
+            continue
+        if cur is not None:
+            if s.startswith(".Lfunc_end") or s.strip().startswith(".size"):
+                cur, name = None, None
+                continue
+            cur.append(s)
+    return funcs
+
+
+def build_cfg(lines):
+    insns, labels, starts = [], {}, []
+    in_asm = False
+    for i, s in enumerate(lines):
+        t = s.strip()
+        if t.startswith(";;#ASMSTART"):
+            in_asm = True
+            continue
+        if t.startswith(";;#ASMEND"):
+            in_asm = False
+            continue
+        m = re.match(r"^(\.LBB\w+):", t)
+        if m:
+            labels[m.group(1)] = len(insns)
+            starts.append(len(insns))
+            continue
+        if t.startswith("; %bb."):
+            starts.append(len(insns))
+            continue
+        if not t or t.startswith((";", ".", "//")):
+            continue
+        insns.append(Insn(len(insns), i, t, in_asm))
+    n = len(insns)
+    succ = defaultdict(list)
+    for ins in insns:
+        if ins.op == "s_endpgm":
+            continue
+        if BRANCH_RE.match(ins.op):
+            tgt = ins.args.split()[0]
+            if tgt in labels:
+                ins.target = labels[tgt]
+                succ[ins.idx].append(labels[tgt])
+            if ins.op != "s_branch" and ins.idx + 1 < n:
+                succ[ins.idx].append(ins.idx + 1)
+        elif ins.idx + 1 < n:
+            succ[ins.idx].append(ins.idx + 1)
+    return insns, succ
+
+
+SOP_RE = re.compile(r"\bs\[(\d+):(\d+)\]|\bs(\d+)\b")
+
+
+def sregs(text):
+    out = []
+    for m in SOP_RE.finditer(text):
+        if m.group(1):
+            out += [int(r) for r in range(int(m.group(1)), int(m.group(2)) + 1)]
+        else:
+            out.append(int(m.group(3)))
+    return out
+
+
+def scalar_step(ins, consts):
+    """Updates the known scalar constants in place for one instruction; returns (branch taken
+    feasible, fall-through feasible). Tracks s_mov_b32/b64 of 0 / -1, vcc from s_and(n2)_b64 vcc,
+    exec, s[..] and scc from s_cmp_lg/eq_u64 s[..], 0; anything else that writes a tracked
+    register (or vcc / scc) forgets it."""
+    op, a = ins.op, ins.args.split(";")[0]
+    ops = [o.strip() for o in a.split(",")]
+    taken, fall = True, True
+
+    def known(regs):
+        vals = [consts.get(("s", r)) for r in regs]
+        return None if (not regs or any(v is None for v in vals)) else all(v == -1 for v in vals) and "ones" or (
+            "zero" if all(v == 0 for v in vals) else "mixed")
+
+    if op.startswith("s_cbranch_"):
+        cond = op[len("s_cbranch_"):]
+        v = consts.get(("vcc",)) if cond in ("vccz", "vccnz") else consts.get(("scc",)) if cond in ("scc0", "scc1") else None
+        if v is not None:
+            t = {"vccz": v == 0, "vccnz": v == 1, "scc0": v == 0, "scc1": v == 1}[cond]
+            taken, fall = t, not t
+        return taken, fall
+    if op in ("s_branch", "s_waitcnt", "s_barrier", "s_nop", "s_setprio", "s_endpgm") or not ops or not ops[0]:
+        return taken, fall
+    dst = ops[0]
+    if op in ("s_mov_b64", "s_mov_b32") and dst.startswith("s") and len(ops) == 2 and ops[1] in ("0", "-1"):
+        for r in sregs(dst):
+            consts[("s", r)] = int(ops[1])
+        return taken, fall
+    if op in ("s_and_b64", "s_andn2_b64") and dst == "vcc" and len(ops) == 3 and ops[1] == "exec":
+        k = known(sregs(ops[2]))
+        consts.pop(("scc",), None)
+        if k in ("ones", "zero"):
+            nz = (k == "ones") if op == "s_and_b64" else (k == "zero")
+            consts[("vcc",)] = 1 if nz else 0
+        else:
+            consts.pop(("vcc",), None)
+        return taken, fall
+    if op in ("s_cmp_lg_u64", "s_cmp_eq_u64") and len(ops) == 2 and ops[1] == "0":
+        k = known(sregs(ops[0]))
+        if k in ("ones", "zero"):
+            nz = k == "ones"
+            consts[("scc",)] = int(nz if op == "s_cmp_lg_u64" else not nz)
+        else:
+            consts.pop(("scc",), None)
+        return taken, fall
+    # generic: forget what this instruction may write (its first operand, vcc, scc)
+    for r in sregs(dst):
+        consts.pop(("s", r), None)
+    if "vcc" in dst or op.startswith("v_cmp") or op.startswith("v_add_co") or op.startswith("v_sub_co"):
+        consts.pop(("vcc",), None)
+    if op.startswith("s_"):
+        consts.pop(("scc",), None)
+    return taken, fall
+
+
+def audit(lines):
+    """Returns (hazards, orphans, asm VMEM count). Forward dataflow of {load: min younger VMEM count
+    over all paths} per instruction; then, per asm load L with destination registers:
+      * its consumers are the asm waits that name its registers (`; bcfft-wait <regs>`, the
+        kernels' wait_b); a consumer reached with L in flight must retire it (>= N younger VMEM
+        instructions on every path, for its vmcnt(N)), else the wait does not cover the load;
+      * an instruction that touches L's registers while L may be in flight, on a path that goes on
+        to one of L's consumers, is a hazard (the compiler read a stale value, or wrote a register
+        the landing load then overwrites);
+      * a touch on a path that never reaches a consumer is counted as an orphan: either the path
+        is infeasible (e.g. the next chunk's fragments are loaded only while there is a next chunk,
+        `cn >= 0`, and the path skips that chunk) or the load is never waited for at all."""
+    insns, succ = build_cfg(lines)
+    if not insns:
+        return [], 0, 0
+    # Path states carry a few known scalar constants, so that the compiler's if / else over a
+    # uniform flag (`s_mov_b64 s[4:5], -1; s_and_b64 vcc, exec, c; s_cbranch_vccz A; <then>;
+    # s_mov_b64 s[4:5], 0; A: s_andn2_b64 vcc, exec, s[4:5]; s_cbranch_vccnz B; <else>`) is not
+    # walked through neither branch (a path on which the x DMA of neither branch issues).
+    # state_in[i] = {consts: {load: min younger count}}, consts a frozenset of (register, value).
+    state_in = {0: {frozenset(): {}}}
+    work = [(0, frozenset())]
+    while work:
+        i, key = work.pop()
+        st = dict(state_in[i][key])
+        consts = dict(key)
+        ins = insns[i]
+        if ins.vmcnt is not None:
+            st = {k: c for k, c in st.items() if c < ins.vmcnt}
+        if ins.vmem:
+            st = {k: min(c + 1, CAP) for k, c in st.items()}
+            if ins.dest and ins.asm:
+                st[i] = 0
+        taken_ok, fall_ok = scalar_step(ins, consts)
+        nkey = frozenset(consts.items())
+        for j in succ[i]:
+            if BRANCH_RE.match(ins.op) and ins.op != "s_branch":
+                ok = (j == ins.target and taken_ok) or (j == i + 1 and fall_ok)
+                if not ok:
+                    continue
+            bucket = state_in.setdefault(j, {})
+            if len(bucket) >= 16 and nkey not in bucket:
+                kk = frozenset()                    # too many splits: forget the constants
+            else:
+                kk = nkey
+            old = bucket.get(kk)
+            if old is None:
+                new = dict(st)
+            else:
+                new = dict(old)
+                for k, c in st.items():
+                    new[k] = min(new.get(k, CAP), c)
+            if old != new:
+                bucket[kk] = new
+                work.append((j, kk))
+    # merge the per-constant states: min over all path classes
+    merged = {}
+    for i, bucket in state_in.items():
+        m = {}
+        for stt in bucket.values():
+            for k, c in stt.items():
+                m[k] = min(m.get(k, CAP), c)
+        merged[i] = m
+    state_in = merged
+    pred = defaultdict(list)
+    for i, js in succ.items():
+        for j in js:
+            pred[j].append(i)
+    consumers = [x for x in insns if x.asm and x.op == "s_waitcnt" and "bcfft-wait" in x.args]
+    cregs = {x.idx: regs_of(x.args.split("bcfft-wait", 1)[1]) for x in consumers}
+    hazards, orphans = [], 0
+    for ld in insns:
+        if not (ld.asm and ld.dest):
+            continue
+        cons = [x for x in consumers if cregs[x.idx] & ld.dest]
+        # instructions from which a consumer of ld is reachable without re-issuing ld
+        back, stack = set(), [x.idx for x in cons]
+        while stack:
+            x = stack.pop()
+            if x in back:
+                continue
+            back.add(x)
+            stack.extend(p for p in pred[x] if p != ld.idx)
+        for x in cons:
+            c = state_in.get(x.idx, {}).get(ld.idx)
+            if c is not None and c < x.vmcnt:
+                hazards.append((ld, x, c, sorted(ld.dest), "wait does not retire the load"))
+        for ins in insns:
+            st = state_in.get(ins.idx)
+            if not st or ld.idx not in st or ins.idx == ld.idx or ins.idx in cregs:
+                continue
+            c = st[ld.idx]
+            if ins.vmcnt is not None and c >= ins.vmcnt:
+                continue
+            ov = ld.dest & (ins.touch - ins.dest if ins.is_load else ins.touch)
+            if not ov:
+                continue
+            if ins.idx in back:
+                hazards.append((ld, ins, c, sorted(ov), "touched in flight"))
+            else:
+                orphans += 1
+    n_asm = sum(1 for x in insns if x.vmem and x.asm)
+    return hazards, orphans, n_asm
+
+
+def fmt_regs(rs):
+    by = defaultdict(list)
+    for f, r in rs:
+        by[f].append(r)
+    return " ".join(f"{f}{min(v)}..{max(v)}" if len(v) > 1 else f"{f}{v[0]}" for f, v in by.items())
+
+
+def audit_file(path, filt=None, verbose=True):
+    bad = 0
+    for name, lines in parse_functions(path).items():
+        if filt and filt not in name:
+            continue
+        hz, orphans, n_asm = audit(lines)
+        if verbose:
+            print(f"{os.path.basename(path)} {name[:90]}: {len(hz)} hazard(s), {n_asm} asm VMEM instructions, "
+                  f"{orphans} touches on consumer-less paths")
+        for ld, use, c, ov, why in hz[:20]:
+            print(f"    {why}: load L{ld.line + 1} {ld.op} {ld.args[:60]}")
+            print(f"      at L{use.line + 1} {'asm ' if use.asm else ''}{use.op} {use.args[:70]}  "
+                  f"[{fmt_regs(ov)}; >= {c} younger VMEM on every path]")
+        bad += len(hz)
+    return bad
+
+
+def build_and_audit(defs):
+    out = "/tmp/vmem_audit"
+    os.makedirs(out, exist_ok=True)
+    srcs = sorted(f for f in os.listdir(os.path.join(ROOT, "llama-fft_amd", "csrc")) if f.endswith(".hip"))
+    bad = 0
+    for f in srcs:
+        s = os.path.join(out, f.replace(".hip", ".s"))
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
+                        f"-I{ROOT}/include", "-ffp-contract=fast", "-fno-slp-vectorize", "--cuda-device-only",
+                        "-S", *defs, os.path.join(ROOT, "llama-fft_amd", "csrc", f), "-o", s],
+                       check=True, stderr=subprocess.DEVNULL)
+        bad += audit_file(s)
+    return bad
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "--build":
+        nbad = build_and_audit(sys.argv[2:])
+    else:
+        nbad = audit_file(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
+    print(f"total hazards: {nbad}")
+    sys.exit(1 if nbad else 0)
