@@ -74,14 +74,32 @@ __device__ __forceinline__ long bf8x8(uint32_t w0, uint32_t w1, uint32_t w2, uin
   return (long)(((uint64_t)hi << 32) | lo);
 }
 
+// e4m3 (round to nearest even) of eight fp16 values times 2^-6, in order, one byte each (an fp8
+// MFMA operand): |X| < 2^14 in the A rows keeps v 2^-6 within e4m3's 448; the product is scaled
+// back by 2^6 where the residual accumulator joins the main one. v_cvt_scalef32_pk_fp8_f16 converts
+// two fp16 values to e4m3(v / scale) with RNE (tools/probe/cvt_fp8.hip, profiles/r06_probe_cvt_fp8.txt)
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+typedef short s16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ long e4m3x8_s6(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  s16x2v lo = {0, 0}, hi = {0, 0};
+  lo = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(lo, __builtin_bit_cast(f16x2v, w0), 64.f, false);
+  lo = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(lo, __builtin_bit_cast(f16x2v, w1), 64.f, true);
+  hi = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(hi, __builtin_bit_cast(f16x2v, w2), 64.f, false);
+  hi = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(hi, __builtin_bit_cast(f16x2v, w3), 64.f, true);
+  return (long)(((uint64_t)__builtin_bit_cast(uint32_t, hi) << 32) | __builtin_bit_cast(uint32_t, lo));
+}
+
 // EP (precise engine, BCFFT_ALGO_DFTP; bit 1: stage-1 table residual, 2: weight residual, 4:
 // stage-3 table residual; 0 = the dft / dftx kernel): every fp16 single term of the dftx kernel
 // gets its rounding residual back through an fp8 MFMA into the same fp32 accumulator:
 //   * the table is F 2^8 in fp16 (kDmFp) and a is scaled 2^15 lower, so D's scale is unchanged;
 //     the residual F 2^8 - kDmFp (|.| <= 2^-3) is e4m3 (kDmFl8) and multiplies a bf8 copy of the
 //     data's fp16 hi term (the high byte: same value range), in the same fp32 accumulator;
-//   * stage 2 adds A(bf8) x e4m3(conj(C) s_o - fp16(conj(C) s_o)) (the lo8 image, streamed from L2
-//     by every wave for its bins, four bins ahead) to the fp16 product's accumulator;
+//   * stage 2 adds A x e4m3(conj(C) s_o - fp16(conj(C) s_o)) (the lo8 image, streamed from L2
+//     by every wave for its bins, four bins ahead): A as e4m3 (RNE) of the fp16 A rows times 2^-6
+//     into an accumulator of its own, joined to the fp16 product's times 2^6 (BCFFT_DFTP_X8 = 1,
+//     the product: worst structured token 2.4e-4, tools/precision_terms.py), or A as bf8 (the
+//     fp16 value's high byte: 2 mantissa bits, truncated) into the same accumulator (= 0: 9.0e-4);
 //   * stage 3 adds e4m3 table residual x bf8(Y hi).
 // The F waves' x DMA (asm, invisible to the compiler's counters) is issued after Ba, once the
 // first lo8 loads of stage 2 have been waited for. Numpy mirror: tests/dm_model.py
@@ -424,6 +442,9 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
 #ifndef BCFFT_DFTP_RING
 #define BCFFT_DFTP_RING 4
 #endif
+#ifndef BCFFT_DFTP_X8
+#define BCFFT_DFTP_X8 1                             // stage-2 residual operand: 1 e4m3 (RNE) of A 2^-6, 0 bf8 of A
+#endif
   constexpr int RING = BCFFT_DFTP_RING;             // bins of lo8 fragments in flight
   typedef u32x4 ClRing[RING][KS];
   auto cl_load = [&](ClRing& clr, int fb) {
@@ -480,9 +501,9 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
     for (int fb = 0; fb < BW; ++fb) {
       const int f = wave * BW + fb;
       if constexpr (EP != 0) a_load(fb);
-      f32x4 acc[NT];
+      f32x4 acc[NT], racc[NT];                      // racc: the weight residual's products (X8 = 1)
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int nt = 0; nt < NT; ++nt) acc[nt] = racc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         uint4 raw = araw[fb % NAR][ks];
@@ -499,18 +520,31 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
           acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, creg[fb][ks][nt], acc[nt], 0, 0, 0);
-        if constexpr ((EP & 2) != 0) {              // + bf8(A) x e4m3 weight residual, same accumulators
-          const long a8 = bf8x8(raw.x, raw.y, raw.z, raw.w);
+        if constexpr ((EP & 2) != 0) {              // + A x e4m3 weight residual
           const u32x4 c8 = clr[fb % RING][ks];
-          acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf8_fp8(a8, (long)(((uint64_t)c8.y << 32) | c8.x), acc[0], 0, 0, 0);
-          acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf8_fp8(a8, (long)(((uint64_t)c8.w << 32) | c8.z), acc[1], 0, 0, 0);
+          const long b0 = (long)(((uint64_t)c8.y << 32) | c8.x), b1 = (long)(((uint64_t)c8.w << 32) | c8.z);
+          if constexpr (BCFFT_DFTP_X8 != 0) {
+            const long a8 = e4m3x8_s6(raw.x, raw.y, raw.z, raw.w);
+            racc[0] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a8, b0, racc[0], 0, 0, 0);
+            racc[1] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a8, b1, racc[1], 0, 0, 0);
+          } else {
+            const long a8 = bf8x8(raw.x, raw.y, raw.z, raw.w);
+            acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf8_fp8(a8, b0, acc[0], 0, 0, 0);
+            acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf8_fp8(a8, b1, acc[1], 0, 0, 0);
+          }
         }
       }
       constexpr float YS = 1.f / 2097152.f;          // 2^-21: |Y| < 2^14 in fp16
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)                // rows 4 yt + {re hi, re lo, im hi, im lo}
       {
-        const float yr = (acc[nt][0] + acc[nt][1]) * YS, yi = (acc[nt][2] + acc[nt][3]) * YS;
+        float yr = acc[nt][0] + acc[nt][1], yi = acc[nt][2] + acc[nt][3];
+        if constexpr ((EP & 2) != 0 && BCFFT_DFTP_X8 != 0) {
+          yr = fmaf(racc[nt][0] + racc[nt][1], 64.f, yr);
+          yi = fmaf(racc[nt][2] + racc[nt][3], 64.f, yi);
+        }
+        yr *= YS;
+        yi *= YS;
         if constexpr (EX) split2(yr, yi, yh[fb][nt], yl[fb][nt]);
         else yh[fb][nt] = pk_rne(yr, yi);
       }

@@ -1010,6 +1010,12 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256k_kernel(
     char* other = lds + (rsel ^ 1) * REGION;
     const bool tile0 = c == 0;
     if (tile0) {
+      // B(0) of this tile (the previous step's stage-2 loads, asm: invisible to the compiler) has
+      // landed before stage 3: its register pressure made hipcc rotate the 16 fragment registers
+      // around stage 3 (v_mov copies of registers an in-flight load still writes; found by
+      // tools/vmem_audit.py). The wait names the fragments, so copies made
+      // after it carry the landed values. Nothing younger is in flight here.
+      wait_b(std::integral_constant<int, 0>{}, breg);
       stage3(other, wrr[wave], mprev >= 0 ? mprev * TT + wave : -1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
     }

@@ -178,6 +178,13 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
   // drain the x DMA issued after them; wait_b (below) is the one wait on them, with the exact
   // number of younger VMEM operations, and it redefines the registers it waited for, so no use
   // can be scheduled above it.
+  // The dependency the compiler cannot see: between load_b1 and wait_b the destination registers
+  // are being written by the memory system, but hipcc treats them as holding their value. It must
+  // not copy, spill or reuse them there. Round 5's late-DMA schedule (-DBCFFT_DMK_LATE_DMA, kept as
+  // the negative control of tests/test_vmem_audit.py) made hipcc rotate all 64 fragment registers
+  // with v_mov copies across the chunk loop: wrong tokens at N = 4090 on the GPU
+  // (profiles/r06_dmk_late_dma_repro.txt). tools/vmem_audit.py checks every
+  // build's ISA for that; wait_b's `; bcfft-wait <regs>` comment names the registers for it.
   auto b_rsrc = [&](int c) {
     return __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint4*>(bimg + ((int64_t)(grp_o * nch + (c < 0 ? 0 : c)) * NW + wave) * FRAGS * 64), 0,

@@ -19,7 +19,9 @@ are checked on the CPU against the oracle before the GPU runs them:
 precise=True mirrors the precise engine (BCFFT_ALGO_DFTP, the kernel's EP = 7 variant): the table
 is F 2^8 in fp16 (kDmFp) and a, d are scaled 2^15 lower; each fp16 single term gets its rounding
 residual back in e4m3 (kDmFl8 for the table, the lo8 image e4m3(conj(C) s_o - fp16(.)) for the
-weights), multiplied by bf8 (the fp16 value's high byte) of the other operand's fp16 terms.
+weights), multiplied by bf8 (the fp16 value's high byte) of the other operand's fp16 terms in
+the table terms, and by e4m3 (RNE) of the aligned X terms in the weight term (x8="e4m3", the
+kernel's BCFFT_DFTP_X8 = 1; x8="bf8" mirrors round 4's form).
 """
 import os
 import re
@@ -151,7 +153,14 @@ def lo8_image(c):
     return out[0], out[1]
 
 
-def dm_forward(x, c, exact=True, single_x=False, head=None, precise=False, terms=(1, 1, 1)):
+def e4m3_s6(v):
+    """The precise engine's stage-2 residual operand (BCFFT_DFTP_X8 = 1): e4m3 (RNE) of the fp16 A
+    values times 2^-6, returned at the values' own scale (the kernel joins that accumulator to the
+    main one times 2^6)."""
+    return e4m3(np.asarray(v, np.float64) / 64.0) * 64.0
+
+
+def dm_forward(x, c, exact=True, single_x=False, head=None, precise=False, terms=(1, 1, 1), x8="e4m3"):
     """x (N, K) float32, c (nO, nI, 128): the kernel's fp32 output (no bias). exact: the
     BCFFT_ALGO_DFTX variant (a, d and Y as hi + lo); else "dft" (one RNE term each). single_x:
     the bf16-I/O kernel of bcfft_dm8.hip, whose X is one RNE fp16 term too.
@@ -222,8 +231,9 @@ def dm_forward(x, c, exact=True, single_x=False, head=None, precise=False, terms
             else:
                 shi, slo = _split16(pk)
             X[16 * hh:16 * hh + 16] = (shi[..., 0] + slo[..., 0]) + 1j * (shi[..., 1] + slo[..., 1])
-            if precise:                        # bf8 commutes with the exact 2^-d alignment below
-                XB[16 * hh:16 * hh + 16] = (bf8(shi[..., 0]) + bf8(slo[..., 0])) + 1j * (bf8(shi[..., 1]) + bf8(slo[..., 1]))
+            if precise:                        # bf8 / e4m3 commute with the exact 2^-d alignment below
+                q = e4m3_s6 if x8 == "e4m3" else bf8
+                XB[16 * hh:16 * hh + 16] = (q(shi[..., 0]) + q(slo[..., 0])) + 1j * (q(shi[..., 1]) + q(slo[..., 1]))
             nsc.append(sx - 7)
         nmin = min(nsc)
         if head is not None:                                      # the running reference

@@ -165,6 +165,30 @@ def scalar_step(ins, consts):
             t = {"vccz": v == 0, "vccnz": v == 1, "scc0": v == 0, "scc1": v == 1}[cond]
             taken, fall = t, not t
         return taken, fall
+    return _scalar_rest(ins, consts, known)
+
+
+def branch_facts(ins, consts, taken):
+    """The facts a conditional branch establishes on the edge it takes (taken=True) or falls
+    through: vcc computed as s_and(n2)_b64 vcc, exec, s[a:b] from a uniform condition s[a:b]
+    (all lanes set or none) tells whether s[a:b] is zero; recorded as ("flag", a) -> 0 / 1, so a
+    later test of the same, unmodified s[a:b] is decided (the compiler's `if (c) A; ...; if (!c) B`
+    over one condition)."""
+    cond = ins.op[len("s_cbranch_"):]
+    sym = consts.get(("vccsym",))
+    if cond not in ("vccz", "vccnz") or sym is None:
+        return
+    reg, neg = sym
+    vcc_nz = (cond == "vccnz") == taken             # the edge implies vcc != 0
+    flag_nz = vcc_nz != neg                          # s_and: vcc != 0 iff s != 0; s_andn2: iff s == 0
+    consts[("flag", reg)] = 1 if flag_nz else 0
+
+
+def _scalar_rest(ins, consts, known):
+    """scalar_step for the non-branch instructions."""
+    op, a = ins.op, ins.args.split(";")[0]
+    ops = [o.strip() for o in a.split(",")]
+    taken, fall = True, True
     if op in ("s_branch", "s_waitcnt", "s_barrier", "s_nop", "s_setprio", "s_endpgm") or not ops or not ops[0]:
         return taken, fall
     dst = ops[0]
@@ -173,13 +197,19 @@ def scalar_step(ins, consts):
             consts[("s", r)] = int(ops[1])
         return taken, fall
     if op in ("s_and_b64", "s_andn2_b64") and dst == "vcc" and len(ops) == 3 and ops[1] == "exec":
-        k = known(sregs(ops[2]))
+        regs = sregs(ops[2])
+        k = known(regs)
         consts.pop(("scc",), None)
+        consts.pop(("vccsym",), None)
+        if k is None and regs and ("flag", regs[0]) in consts:
+            k = "ones" if consts[("flag", regs[0])] else "zero"
         if k in ("ones", "zero"):
             nz = (k == "ones") if op == "s_and_b64" else (k == "zero")
             consts[("vcc",)] = 1 if nz else 0
         else:
             consts.pop(("vcc",), None)
+            if regs:
+                consts[("vccsym",)] = (regs[0], op == "s_andn2_b64")
         return taken, fall
     if op in ("s_cmp_lg_u64", "s_cmp_eq_u64") and len(ops) == 2 and ops[1] == "0":
         k = known(sregs(ops[0]))
@@ -189,17 +219,26 @@ def scalar_step(ins, consts):
         else:
             consts.pop(("scc",), None)
         return taken, fall
-    # generic: forget what this instruction may write (its first operand, vcc, scc)
+    # generic: forget what this instruction may write (its first operand, vcc, scc); compares
+    # (s_cmp*, s_bitcmp*) write only scc
+    if op.startswith(("s_cmp", "s_bitcmp")):
+        consts.pop(("scc",), None)
+        return taken, fall
     for r in sregs(dst):
         consts.pop(("s", r), None)
+        consts.pop(("flag", r), None)
+        sym = consts.get(("vccsym",))
+        if sym and sym[0] == r:
+            consts.pop(("vccsym",), None)
     if "vcc" in dst or op.startswith("v_cmp") or op.startswith("v_add_co") or op.startswith("v_sub_co"):
         consts.pop(("vcc",), None)
+        consts.pop(("vccsym",), None)
     if op.startswith("s_"):
         consts.pop(("scc",), None)
     return taken, fall
 
 
-def audit(lines):
+def audit(lines, forward=False):
     """Returns (hazards, orphans, asm VMEM count). Forward dataflow of {load: min younger VMEM count
     over all paths} per instruction; then, per asm load L with destination registers:
       * its consumers are the asm waits that name its registers (`; bcfft-wait <regs>`, the
@@ -212,6 +251,8 @@ def audit(lines):
         is infeasible (e.g. the next chunk's fragments are loaded only while there is a next chunk,
         `cn >= 0`, and the path skips that chunk) or the load is never waited for at all."""
     insns, succ = build_cfg(lines)
+    if forward:                                     # one loop iteration: no back edges
+        succ = defaultdict(list, {i: [j for j in js if j > i] for i, js in succ.items()})
     if not insns:
         return [], 0, 0
     # Path states carry a few known scalar constants, so that the compiler's if / else over a
@@ -219,6 +260,8 @@ def audit(lines):
     # s_mov_b64 s[4:5], 0; A: s_andn2_b64 vcc, exec, s[4:5]; s_cbranch_vccnz B; <else>`) is not
     # walked through neither branch (a path on which the x DMA of neither branch issues).
     # state_in[i] = {consts: {load: min younger count}}, consts a frozenset of (register, value).
+    consumers = [x for x in insns if x.asm and x.op == "s_waitcnt" and "bcfft-wait" in x.args]
+    cregs = {x.idx: regs_of(x.args.split("bcfft-wait", 1)[1]) for x in consumers}
     state_in = {0: {frozenset(): {}}}
     work = [(0, frozenset())]
     while work:
@@ -228,6 +271,8 @@ def audit(lines):
         ins = insns[i]
         if ins.vmcnt is not None:
             st = {k: c for k, c in st.items() if c < ins.vmcnt}
+        if i in cregs:                              # the wait that names a load's registers ends its
+            st = {k: c for k, c in st.items() if not (insns[k].dest & cregs[i])}   # window (its count: below)
         if ins.vmem:
             st = {k: min(c + 1, CAP) for k, c in st.items()}
             if ins.dest and ins.asm:
@@ -239,6 +284,9 @@ def audit(lines):
                 ok = (j == ins.target and taken_ok) or (j == i + 1 and fall_ok)
                 if not ok:
                     continue
+                ec = dict(consts)
+                branch_facts(ins, ec, j == ins.target)
+                nkey = frozenset(ec.items())
             bucket = state_in.setdefault(j, {})
             if len(bucket) >= 16 and nkey not in bucket:
                 kk = frozenset()                    # too many splits: forget the constants
@@ -267,8 +315,6 @@ def audit(lines):
     for i, js in succ.items():
         for j in js:
             pred[j].append(i)
-    consumers = [x for x in insns if x.asm and x.op == "s_waitcnt" and "bcfft-wait" in x.args]
-    cregs = {x.idx: regs_of(x.args.split("bcfft-wait", 1)[1]) for x in consumers}
     hazards, orphans = [], 0
     for ld in insns:
         if not (ld.asm and ld.dest):
@@ -304,6 +350,51 @@ def audit(lines):
     return hazards, orphans, n_asm
 
 
+def steady_loop(insns, succ):
+    """Instruction set of the smallest natural loop holding both an asm load with register
+    destinations and a consumer wait: the streamed-weight kernels' chunk / step loop."""
+    pred = defaultdict(list)
+    for i, js in succ.items():
+        for j in js:
+            pred[j].append(i)
+    best = set()
+    for i, js in succ.items():
+        for h in js:
+            if h > i:
+                continue
+            body, stack = {h}, [i]
+            while stack:
+                x = stack.pop()
+                if x in body:
+                    continue
+                body.add(x)
+                stack.extend(pred[x])
+            if (any(insns[x].asm and insns[x].dest for x in body)
+                    and any(insns[x].asm and "bcfft-wait" in insns[x].args for x in body)
+                    and (not best or len(body) < len(best))):
+                best = body
+    return best
+
+
+def check(lines):
+    """The two verdicts the tests assert, per kernel (both free of the dataflow's infeasible-path
+    reports):
+      * within one iteration (no back edges): no instruction touches the registers of an asm load
+        before a wait that names and retires them;
+      * across iterations: no instruction inside the steady-state loop touches them while the
+        load may be in flight.
+    Returns (within-iteration touches, steady-loop touches, unretired-wait reports (information:
+    the path-insensitive count can take a loop that always runs twice through once))."""
+    fwd, _, _ = audit(lines, forward=True)
+    full, _, _ = audit(lines)
+    insns, succ = build_cfg(lines)
+    loop = steady_loop(insns, succ)
+    t_fwd = [h for h in fwd if h[4] == "touched in flight"]
+    t_loop = [h for h in full if h[4] == "touched in flight" and h[1].idx in loop]
+    waits = [h for h in full if h[4] != "touched in flight"]
+    return t_fwd, t_loop, waits
+
+
 def fmt_regs(rs):
     by = defaultdict(list)
     for f, r in rs:
@@ -312,35 +403,42 @@ def fmt_regs(rs):
 
 
 def audit_file(path, filt=None, verbose=True):
+    """check() per kernel of a listing; returns the number of register touches in flight."""
     bad = 0
     for name, lines in parse_functions(path).items():
         if filt and filt not in name:
             continue
-        hz, orphans, n_asm = audit(lines)
+        t_fwd, t_loop, waits = check(lines)
+        n_asm = sum(1 for s in lines if "buffer_load" in s) if verbose else 0
         if verbose:
-            print(f"{os.path.basename(path)} {name[:90]}: {len(hz)} hazard(s), {n_asm} asm VMEM instructions, "
-                  f"{orphans} touches on consumer-less paths")
-        for ld, use, c, ov, why in hz[:20]:
+            print(f"{os.path.basename(path)} {name[:80]}: {len(t_fwd)} within-iteration / {len(t_loop)} "
+                  f"steady-loop register touches in flight; {len(waits)} unretired-wait reports (information)")
+        for ld, use, c, ov, why in (t_fwd + t_loop)[:12]:
             print(f"    {why}: load L{ld.line + 1} {ld.op} {ld.args[:60]}")
             print(f"      at L{use.line + 1} {'asm ' if use.asm else ''}{use.op} {use.args[:70]}  "
                   f"[{fmt_regs(ov)}; >= {c} younger VMEM on every path]")
-        bad += len(hz)
+        bad += len(t_fwd) + len(t_loop)
     return bad
+
+
+# translation units that issue VMEM loads into registers from inline asm (the streamed-weight kernels)
+ASM_LOAD_TUS = ("bcfft_dmk", "bcfft_dm256", "bcfft_dm64k")
+
+
+def compile_isa(tu, defs=(), out_dir="/tmp/vmem_audit"):
+    """hipcc -S of one product translation unit for gfx950 (the product's flags); returns the path."""
+    os.makedirs(out_dir, exist_ok=True)
+    tag = "".join(d.replace("-D", "_").replace("=", "") for d in defs)
+    s = os.path.join(out_dir, f"{tu}{tag}.s")
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
+                    f"-I{ROOT}/include", "-ffp-contract=fast", "-fno-slp-vectorize", "--cuda-device-only",
+                    "-S", *defs, os.path.join(ROOT, "llama-fft_amd", "csrc", f"{tu}.hip"), "-o", s],
+                   check=True, stderr=subprocess.DEVNULL)
+    return s
 
 
 def build_and_audit(defs):
-    out = "/tmp/vmem_audit"
-    os.makedirs(out, exist_ok=True)
-    srcs = sorted(f for f in os.listdir(os.path.join(ROOT, "llama-fft_amd", "csrc")) if f.endswith(".hip"))
-    bad = 0
-    for f in srcs:
-        s = os.path.join(out, f.replace(".hip", ".s"))
-        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
-                        f"-I{ROOT}/include", "-ffp-contract=fast", "-fno-slp-vectorize", "--cuda-device-only",
-                        "-S", *defs, os.path.join(ROOT, "llama-fft_amd", "csrc", f), "-o", s],
-                       check=True, stderr=subprocess.DEVNULL)
-        bad += audit_file(s)
-    return bad
+    return sum(audit_file(compile_isa(tu, defs)) for tu in ASM_LOAD_TUS)
 
 
 if __name__ == "__main__":
