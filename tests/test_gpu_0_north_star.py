@@ -179,8 +179,15 @@ def test_structured_weights_per_block_and_token(dev, monkeypatch, algo, xdt):
     assert per_block.max() < tol, (int(per_block.argmax()), per_block.max())
     assert pt_cond.max() < tol, (int(pt_cond.argmax()), pt_cond.max())
     assert pt.max() < 50 * tol                        # gross-error guard on the raw figure
-    if algo in ("dftp", "precise"):                   # the precise engine: raw per token within the north star
-        assert pt.max() < TOKEN_TOL, (int(pt.argmax()), pt.max())
+    if algo in ("dftp", "precise"):
+        # the precise engine: RAW per token within the north star, with margin (measured 1.8e-4:
+        # the weight residual against e4m3 (RNE) of X; 8.8e-4 with round 4's bf8 operand)
+        assert pt.max() < TOKEN_TOL / 2, (int(pt.argmax()), pt.max())
+    elif algo in ("auto", "dftx") and xdt == "float32":
+        # NOT per-token faithful on cancelling tokens (measured 5.9e-3 raw at x26-54 cancellation):
+        # the weight spectra's single fp16 term. Pinned here so a change
+        # either way shows; BCFFT_PRECISE=1 (dftp) is the engine that meets 1e-3 per token raw.
+        assert 1e-3 < pt.max() < 1e-2, pt.max()
 
 
 DFT_GOLDEN = [nm for nm in names("fwd_") if nm.startswith(("fwd_4096sq_b128", "fwd_up_4096x11008_b128"))]
