@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "bcfft.h"
+#include "bcfft_analysis.h"
 
 namespace bcfft {
 
@@ -191,38 +192,6 @@ __device__ __forceinline__ void wait_vmcnt() {
 // workgroup rendezvous on LDS: own LDS traffic complete, then s_barrier; VMEM stays in flight
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-#if defined(BCFFT_ABLATE) || defined(BCFFT_STAMPS)
-// analysis builds only (make ablate / make stamps): phase switches set through bcfft_set_ablation(), and a
-// per-wave phase timeline (s_memtime at STAMP points) when bcfft_set_stamps() gave a buffer
-// (static: each translation unit has its own copy and its own setter). ANALYSIS_INIT reads both
-// ONCE per kernel into scalars: a per-use read would be a global load + s_waitcnt vmcnt(0) that
-// drains every in-flight store and DMA, i.e. the measurement would serialise the kernel.
-static __device__ int g_ablate;
-static __device__ unsigned long long* g_stamps;
-#define ANALYSIS_INIT                                                                          \
-  const int ablate_flags_ = __builtin_amdgcn_readfirstlane(g_ablate);                          \
-  unsigned long long* const stamps_ = g_stamps;                                                \
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory")
-#ifdef BCFFT_ABLATE
-#define ABLATE(bit) (ablate_flags_ & (bit))
-#else                                  // stamps-only build: the product's control flow, timed
-#define ABLATE(bit) 0
-#endif
-#define STAMP_SLOTS 64
-#define STAMP(id)                                                                              \
-  do {                                                                                         \
-    if (stamps_ && (threadIdx.x & 63) == 0) {                                                  \
-      unsigned long long t_;                                                                   \
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_) :: "memory");           \
-      stamps_[((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)) \
-          * STAMP_SLOTS + (id)] = t_;                                                          \
-    }                                                                                          \
-  } while (0)
-#else
-#define ANALYSIS_INIT do {} while (0)
-#define ABLATE(bit) 0
-#define STAMP(id) do {} while (0)
-#endif
 
 // ------------------------------------------------------------------ complex helpers
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
@@ -495,14 +464,10 @@ __device__ __forceinline__ GroupMap group_map(int n_groups) {
 // groups. It is not trimmed to a multiple of 8 x groups. Trimming 256 CUs to 240 for 3 groups
 // cut the HBM reads at 4096 -> 11008 bf16 from 196 to 74 MB (PMC), but it did not save time:
 // these kernels are compute-bound. In one A/B session
-// (`BCFFT_XCD_TRIM`, profiles/r02_ab_xcd_map.log) config 2 was level (83-86 us either way),
+// (profiles/r02_ab_xcd_map.log; the trim is in the git history of this file) config 2 was level (83-86 us either way),
 // while the fused gate/up went from 180 to 189 us and b = 64 4096 -> 11008 from 136 to 140 us.
 inline int64_t group_grid(int64_t cus, int groups, int64_t n_mtiles) {
   int64_t total = cus;
-#ifdef BCFFT_XCD_TRIM                               // analysis builds only
-  const int64_t xt = cus / (8 * groups) * (8 * groups);
-  if (groups > 1 && n_mtiles * groups >= cus && xt * 16 >= cus * 15) total = xt;
-#endif
   if (total > groups * n_mtiles) total = groups * n_mtiles;
   if (total < groups) total = groups;
   return total;
@@ -525,9 +490,7 @@ struct SpecLayout {
   int n_chunk, n_out_pad, stat_groups, stat_pieces;
 };
 int device_cu_count();         // CUs of the current device (bcfft_stat.hip)
-#ifndef BCFFT_MFMA_MAXB
-#define BCFFT_MFMA_MAXB 128          // largest block size with a split-bf16 MFMA image
-#endif
+constexpr int BCFFT_MFMA_MAXB = 128;   // largest block size with a split-bf16 MFMA image
 __host__ __device__ inline int mfma_out_per_wg(int b) { return 4096 / b; }   // 16 * NTL
 // stationary-weight kernel geometries: fp16 B fragments of 32 output blocks x all inputs fit
 // 128 VGPRs per lane of 8 waves (K <= 4096), and the A image swizzle needs >= 8 block quads
@@ -613,13 +576,9 @@ inline int64_t sn_workgroups(int64_t n_tokens, int n_out) { return (n_tokens + 3
 inline bool sn_pays(int64_t n_tokens, int n_out) {
   return n_tokens > 0 && sn_workgroups(n_tokens, n_out) <= device_cu_count();
 }
-// 2-token tiles (launch_forward_sn) while their workgroups also fit one round; BCFFT_SN_TT2=0
-// builds the 4-token tiles only
-#ifndef BCFFT_SN_TT2
-#define BCFFT_SN_TT2 1
-#endif
+// 2-token tiles (launch_forward_sn) while their workgroups also fit one round
 inline bool sn_tt2(int64_t n_tokens, int n_out) {
-  return BCFFT_SN_TT2 != 0 && n_tokens > 0 && (n_tokens + 1) / 2 * ((n_out + 15) / 16) <= device_cu_count();
+  return n_tokens > 0 && (n_tokens + 1) / 2 * ((n_out + 15) / 16) <= device_cu_count();
 }
 // DFT-on-MFMA kernel (bcfft_dm.hip): the STAT image's geometry subset b = 128, K = 4096
 bool dm_eligible(int n_in, int b);
@@ -671,16 +630,12 @@ const char* dm256_kernel_name(int64_t n, int n_in, int n_out);   // the kernel l
 void launch_forward_dm256_glu(const void* x, int64_t n, int n_gate, const void* spec, void* h, hipStream_t s);
 // b = 64, K > 4096 (up to 255 input blocks), bf16 x and bf16 y (bcfft_dm64k.hip)
 bool dm64k_eligible(int n_in, int b, int xdt, bool yf32);
-#ifndef BCFFT_DM64K_MIN_TOKENS
-#define BCFFT_DM64K_MIN_TOKENS 128   // AUTO picks the b = 64 streamed-weight kernel from this many tokens
-#endif
+constexpr int BCFFT_DM64K_MIN_TOKENS = 128;   // AUTO picks the b = 64 streamed-weight kernel from this many tokens
 void launch_forward_dm64k(const void* x, int64_t n, int n_in, int n_out, const void* spec, const void* bias,
                           int bias_dt, void* y, hipStream_t s);
 // streamed-weight DFT kernel (bcfft_dmk.hip): b = 128, K > 4096, bf16 x and bf16 y
 bool dmk_eligible(int n_in, int b, int xdt, bool yf32);
-#ifndef BCFFT_DMK_MIN_TOKENS
-#define BCFFT_DMK_MIN_TOKENS 1       // AUTO picks the streamed-weight kernel from this many tokens
-#endif
+constexpr int BCFFT_DMK_MIN_TOKENS = 1;       // AUTO picks the streamed-weight kernel from this many tokens
 void launch_forward_dmk(const void* x, int64_t n, int n_in, int n_out, const void* spec, const void* bias,
                         int bias_dt, void* y, hipStream_t s);
 void launch_dmk_image(int n_out, int n_in, void* spec, hipStream_t s);

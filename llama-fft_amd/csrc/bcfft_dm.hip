@@ -97,34 +97,18 @@ __device__ __forceinline__ long e4m3x8_s6(uint32_t w0, uint32_t w1, uint32_t w2,
 //     data's fp16 hi term (the high byte: same value range), in the same fp32 accumulator;
 //   * stage 2 adds A x e4m3(conj(C) s_o - fp16(conj(C) s_o)) (the lo8 image, streamed from L2
 //     by every wave for its bins, four bins ahead): A as e4m3 (RNE) of the fp16 A rows times 2^-6
-//     into an accumulator of its own, joined to the fp16 product's times 2^6 (BCFFT_DFTP_X8 = 1,
-//     the product: worst structured token 2.4e-4, tools/precision_terms.py), or A as bf8 (the
-//     fp16 value's high byte: 2 mantissa bits, truncated) into the same accumulator (= 0: 9.0e-4);
+//     into an accumulator of its own, joined to the fp16 product's times 2^6 (worst
+//     structured token 2.4e-4, tools/precision_terms.py; A as bf8, the fp16 value's high byte,
+//     gave 9.0e-4: profiles/r06_precise_probe.txt);
 //   * stage 3 adds e4m3 table residual x bf8(Y hi).
 // The F waves' x DMA (asm, invisible to the compiler's counters) is issued after Ba, once the
 // first lo8 loads of stage 2 have been waited for. Numpy mirror: tests/dm_model.py
 // (precise=True); error ~1e-5 relative (north star 1e-3), per token ~1e-5 x its cancellation.
-#ifndef BCFFT_DM_LB
-#define BCFFT_DM_LB 2
-#endif
-// schedule switches of bc_forward_dm_kernel (defaults = the product; 0 for A/B builds)
-#ifndef BCFFT_DM_LATE_W
-#define BCFFT_DM_LATE_W 1                           // weight fragments waited for after the first stage 1
-#endif
-#ifndef BCFFT_DM_EARLY_X
-#define BCFFT_DM_EARLY_X 1                          // iteration 0: the I waves stream the next tile's x at once
-#endif
-#ifndef BCFFT_DM_SPLIT_FD
-#define BCFFT_DM_SPLIT_FD 1                         // pipeline fill and drain split over both waves of a slot
-#endif
-#ifndef BCFFT_DM_XWAIT
-#define BCFFT_DM_XWAIT 1                            // steady-state stage 1 waits for each half of x on its own
-#endif
 // BM: bias handling, -1 = by the runtime bias_dt (dft / dftx); 0 = none, 1 = fp32 bias, 2 = 16-bit
 // bias, its 4 consecutive values per lane read by one buffer load (the precise engine: the general
 // per-element path's address registers do not fit beside its residual operands)
 template <int XT, bool YF32, bool EX, bool GLU, int EP = 0, int BM = -1>
-__global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
+__global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_out, const uint32_t* __restrict__ stat,
     const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv,
     const uint4* __restrict__ lo8) {
@@ -135,25 +119,22 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
   constexpr int ESY = Y32 ? 4 : 2;
   constexpr int NPIECE = BW * KS * NT;
   constexpr int NDMA = K * ES / 1024;               // 1-KiB LDS-DMA pieces per token
-  constexpr bool LATE_W = BCFFT_DM_LATE_W != 0;
-  constexpr bool EARLY_X = BCFFT_DM_EARLY_X != 0;
+  // LATE_W: the weight fragments are waited for after the first stage 1; EARLY_X: in iteration 0
+  // the I waves stream the next tile's x at once (both measured wins)
+  constexpr bool LATE_W = true;
+  constexpr bool EARLY_X = true;
   // FILL_SPLIT / DRAIN_SPLIT: the pipeline's first P1 has no stage 3 and its last no stage 1, so
   // half the waves would idle through them: the first stage 1 runs one half of each token on its
   // F wave and the other on its I wave (fp32 x: the halves are in place independently; the
   // prologue's x DMA is split the same way), and the last stage 3 one N-tile on each
   // (not in the precise engine: its residual operands leave no registers for the split paths)
-  constexpr bool FILL_SPLIT = BCFFT_DM_SPLIT_FD != 0 && LATE_W && ES == 4 && EP == 0;
-  constexpr bool DRAIN_SPLIT = BCFFT_DM_SPLIT_FD != 0 && !GLU && EP == 0;
+  constexpr bool FILL_SPLIT = LATE_W && ES == 4 && EP == 0;
+  constexpr bool DRAIN_SPLIT = !GLU && EP == 0;
   // (round 4 measured and rejected other x-DMA placements and role splits: DESIGN.md section 8c,
   // item 8, with their A/B logs; their switches are in the git history of this file)
 
   ANALYSIS_INIT;
   bool sub_on = false;                              // sub-phase stamps (analysis builds: iteration 4)
-#ifdef BCFFT_MARKS
-#define SUBSTAMP(id) do { asm volatile(";MARK s" #id); if (sub_on) STAMP(id); } while (0)
-#else
-#define SUBSTAMP(id) do { if (sub_on) STAMP(id); } while (0)
-#endif
   __shared__ __attribute__((aligned(16))) char lds[EP ? LDS_BYTES_EP : LDS_BYTES];
   int* wsc = reinterpret_cast<int*>(lds + SC_OFF);
 
@@ -403,9 +384,6 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
               const s16x4 rl = rlv[4 * pr + mt];
               acc[4 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_bf8(__builtin_bit_cast(long, rl), pr ? b8d : b8a,
                                                                            acc[4 * pr + mt], 0, 0, 0);
-#if defined(BCFFT_DFTP_DBG) && BCFFT_DFTP_DBG == 5
-              asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-#endif
             }
           }
       }
@@ -439,13 +417,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
   const __amdgpu_buffer_rsrc_t clrs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint4*>(lo8) + ((EP & 2) ? (int64_t)(grp_o * NW + wave) * BW * KS * 64 : 0), 0,
       (EP & 2) ? BW * KS * 1024 : 0, 0x00020000);
-#ifndef BCFFT_DFTP_RING
-#define BCFFT_DFTP_RING 4
-#endif
-#ifndef BCFFT_DFTP_X8
-#define BCFFT_DFTP_X8 1                             // stage-2 residual operand: 1 e4m3 (RNE) of A 2^-6, 0 bf8 of A
-#endif
-  constexpr int RING = BCFFT_DFTP_RING;             // bins of lo8 fragments in flight
+  constexpr int RING = 4;                           // bins of lo8 fragments in flight
   typedef u32x4 ClRing[RING][KS];
   auto cl_load = [&](ClRing& clr, int fb) {
     asm volatile("" ::: "memory");                  // keep the loads here: hoisted, they would hold
@@ -501,7 +473,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
     for (int fb = 0; fb < BW; ++fb) {
       const int f = wave * BW + fb;
       if constexpr (EP != 0) a_load(fb);
-      f32x4 acc[NT], racc[NT];                      // racc: the weight residual's products (X8 = 1)
+      f32x4 acc[NT], racc[NT];                      // racc: the weight residual's products
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) acc[nt] = racc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -523,15 +495,9 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
         if constexpr ((EP & 2) != 0) {              // + A x e4m3 weight residual
           const u32x4 c8 = clr[fb % RING][ks];
           const long b0 = (long)(((uint64_t)c8.y << 32) | c8.x), b1 = (long)(((uint64_t)c8.w << 32) | c8.z);
-          if constexpr (BCFFT_DFTP_X8 != 0) {
-            const long a8 = e4m3x8_s6(raw.x, raw.y, raw.z, raw.w);
-            racc[0] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a8, b0, racc[0], 0, 0, 0);
-            racc[1] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a8, b1, racc[1], 0, 0, 0);
-          } else {
-            const long a8 = bf8x8(raw.x, raw.y, raw.z, raw.w);
-            acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf8_fp8(a8, b0, acc[0], 0, 0, 0);
-            acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf8_fp8(a8, b1, acc[1], 0, 0, 0);
-          }
+          const long a8 = e4m3x8_s6(raw.x, raw.y, raw.z, raw.w);
+          racc[0] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a8, b0, racc[0], 0, 0, 0);
+          racc[1] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a8, b1, racc[1], 0, 0, 0);
         }
       }
       constexpr float YS = 1.f / 2097152.f;          // 2^-21: |Y| < 2^14 in fp16
@@ -539,7 +505,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
       for (int nt = 0; nt < NT; ++nt)                // rows 4 yt + {re hi, re lo, im hi, im lo}
       {
         float yr = acc[nt][0] + acc[nt][1], yi = acc[nt][2] + acc[nt][3];
-        if constexpr ((EP & 2) != 0 && BCFFT_DFTP_X8 != 0) {
+        if constexpr ((EP & 2) != 0) {
           yr = fmaf(racc[nt][0] + racc[nt][1], 64.f, yr);
           yi = fmaf(racc[nt][2] + racc[nt][3], 64.f, yi);
         }
@@ -554,9 +520,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
       if constexpr ((EP & 2) != 0) {
         __builtin_amdgcn_sched_barrier(0);
         if (fb + RING < BW) cl_load(clr, fb + RING);
-#ifndef BCFFT_DFTP_NO_SCHED_BARRIER
         __builtin_amdgcn_sched_barrier(0);          // one bin at a time: the overlapped schedule spills
-#endif
       }
     }
     char* yb = region + yt * SLOT + wave * 1024 + 16 * (ml & 15);
@@ -845,7 +809,7 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
     // inlined copies, the first steady-state stage 1 of every CU missed the instruction cache
     // together: ~5 k cycles, profiles/r05y_timeline_dm_nofd.txt)
     const bool fill = FILL_SPLIT && it == 0;
-    constexpr bool XW = BCFFT_DM_XWAIT != 0 && ES == 4 && EP == 0;
+    constexpr bool XW = ES == 4 && EP == 0;         // steady-state stage 1 waits for each half of x on its own
     if (have_f && (fill || fwave)) {
       if (fill) {                                   // fill: both waves of a slot, one half each
         if (!fwave && early) wait_vmcnt<NPIECE + NDMA>();   // own half of tile 0's x (prologue)
@@ -895,9 +859,6 @@ __global__ __launch_bounds__(512, BCFFT_DM_LB) void bc_forward_dm_kernel(
 }  // namespace bcfft
 
 namespace {
-#ifndef BCFFT_DFTP_EP
-#define BCFFT_DFTP_EP 7                             // analysis builds: which residual terms the precise engine adds
-#endif
 template <int XT, bool YF32, bool EX, bool GLU = false, int EP = 0, int BM = -1>
 void launch_dm(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt, void* y,
                hipStream_t s) {
@@ -913,17 +874,12 @@ void launch_dm(const void* x, int64_t n, int n_out, const void* spec, const void
 }
 }  // namespace
 
-#if defined(BCFFT_ABLATE) || defined(BCFFT_STAMPS)
 // analysis builds only: stamp buffer of bc_forward_dm_kernel (this TU's copy). Slots per wave:
 // 0 start | per M-tile it (base 1 + 6 min(it, 8)): +0 loop top, +1 stage 1 / stage 3 done,
 // +2 after Ba, +3 DMA issued (F waves), +4 stage 2 done, +5 after Bb | 55-62 sub-phases of
 // iteration 4 (F waves, per half: x read, scale, MFMAs, X written; I waves: Y read, DMA issued,
 // per N-tile computed + stored, DMA 2 issued) | 63 end
-extern "C" int bcfft_set_stamps_dm(void* buf) {
-  unsigned long long* p = (unsigned long long*)buf;
-  return hipMemcpyToSymbol(HIP_SYMBOL(bcfft::g_stamps), &p, sizeof(p)) == hipSuccess ? 0 : BCFFT_ERR_HIP;
-}
-#endif
+BCFFT_STAMPS_SETTER(dm)
 
 namespace bcfft {
 bool dm_eligible(int n_in, int b) { return b == 128 && n_in == 32; }
@@ -941,7 +897,7 @@ bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, int mode, const void
   // (a 16-bit bias on fp32 x runs DFTX too: the precise engine's BM = 2 instantiation computed
   // wrong outputs on gfx950)
   if (mode == 2 && yf32 && xdt == BCFFT_F32 && (bias_dt == BCFFT_NONE || bias_dt == BCFFT_F32)) {
-    constexpr int P = BCFFT_DFTP_EP;
+    constexpr int P = 7;                            // all three residual terms
     if (bias_dt == BCFFT_NONE) launch_dm<BCFFT_F32, true, true, false, P, 0>(x, n, n_out, spec, bias, bias_dt, y, s);
     else launch_dm<BCFFT_F32, true, true, false, P, 1>(x, n, n_out, spec, bias, bias_dt, y, s);
     return true;
@@ -958,18 +914,14 @@ bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, int mode, const void
   (YF ? (exact ? BCFFT_DM_LAUNCH_EX(XT, true) : BCFFT_DM_LAUNCH_EX(XT, false))                             \
       : (exact ? launch_dm<XT, YF, true>(x, n, n_out, spec, bias, bias_dt, y, s)                          \
                : launch_dm<XT, YF, false>(x, n, n_out, spec, bias, bias_dt, y, s)))
-#ifndef BCFFT_NO_DM8
   if (!exact && dm8_eligible(n_in, b, xdt, yf32)) {  // bf16 I/O: 8 tokens per tile
-#ifndef BCFFT_NO_DMG
     if (dmg_eligible(n_in, b, xdt, yf32, n_out, false) && multigroup_pays(n, 3)) {   // x transformed once (bcfft_dmg.hip)
       launch_forward_dmg(x, n, n_out, spec, bias, bias_dt, y, false, s);
       return true;
     }
-#endif
     launch_forward_dm8(x, n, n_out, spec, bias, bias_dt, y, false, s);   // bcfft_dm8.hip
     return true;
   }
-#endif
   if (xdt == BCFFT_F32) BCFFT_DM_LAUNCH(BCFFT_F32, true);
   else if (xdt == BCFFT_F16 && yf32) BCFFT_DM_LAUNCH(BCFFT_F16, true);
   else if (xdt == BCFFT_F16) launch_dm<BCFFT_F16, false, true>(x, n, n_out, spec, bias, bias_dt, y, s);
@@ -986,7 +938,7 @@ bool launch_forward_dm_glu(int b, int n_in, int xdt, int mode, const void* x, in
   if (!dm_eligible(n_in, b)) return false;
   const bool exact = mode >= 1;
   if (mode == 2 && xdt == BCFFT_F32) {             // precise engine: fp32 h only (16-bit h: DFTX)
-    launch_dm<BCFFT_F32, true, true, true, BCFFT_DFTP_EP, 0>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
+    launch_dm<BCFFT_F32, true, true, true, 7, 0>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
     return true;
   }
   if (xdt == BCFFT_F32) {
@@ -996,15 +948,9 @@ bool launch_forward_dm_glu(int b, int n_in, int xdt, int mode, const void* x, in
     launch_dm<BCFFT_F16, false, true, true>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
   } else {
     if (exact) launch_dm<BCFFT_BF16, false, true, true>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
-#ifndef BCFFT_NO_DM8
-#ifndef BCFFT_NO_DMG
     else if (dmg_eligible(n_in, b, xdt, false, n_gate, true) && multigroup_pays(n, 5))
       launch_forward_dmg(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, true, s);   // x transformed once per tile
-#endif
     else launch_forward_dm8(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, true, s);   // 8 tokens per tile
-#else
-    else launch_dm<BCFFT_BF16, false, false, true>(x, n, n_gate, spec, nullptr, BCFFT_NONE, h, s);
-#endif
   }
   return true;
 }

@@ -467,14 +467,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256_kernel(
     const int par = it & 1;
     const bool have = m < n_mtiles;
     const bool pf = m + gstride < n_mtiles;
-#ifndef BCFFT_DM256_MIX
-#define BCFFT_DM256_MIX 1
-#endif
-#ifndef BCFFT_DM256_YPRIO
-#define BCFFT_DM256_YPRIO 1
-#endif
-    if (!BCFFT_DM256_MIX || (wave < 4 && it > 0 && have)) {
-      // stage 3 of the previous tile, the next tile's x DMA, then stage 1 (with MIX: waves 0-3)
+    if (wave < 4 && it > 0 && have) {
+      // waves 0-3: stage 3 of the previous tile, the next tile's x DMA, then stage 1
       if (it > 0) stage3(other, par ^ 1, m - gstride);
       if (pf) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's staging reads are done
@@ -490,15 +484,15 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256_kernel(
       }
       stage1(region, par);
     } else {
-      // MIX (waves 4-7, and every wave of the first and last iterations): stage 1 first, at a
+      // waves 4-7, and every wave of the first and last iterations): stage 1 first, at a
       // higher priority than the partner wave's stage 3 (bcfft_dm8.hip's mixed order and YPRIO):
       // 39.2 -> 36.8 us over six interleaved passes, the order alone 38.7
       // (profiles/r05ad_ab_dm256_mix_yprio.log)
       if (have) {
         wait_vmcnt<0>();                            // this wave's x (issued an iteration ago)
-        if (BCFFT_DM256_YPRIO) __builtin_amdgcn_s_setprio(BCFFT_DM256_YPRIO);
+        __builtin_amdgcn_s_setprio(1);
         stage1(region, par);
-        if (BCFFT_DM256_YPRIO) __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(0);
       }
       if (it > 0) stage3(other, par ^ 1, m - gstride);
       if (pf) {
@@ -529,10 +523,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm256_kernel(
 namespace d256 {
 constexpr int HEAD = 4;
 // wave priority falling through stage 1 (1) and stage 2 (2): set_prio, bcfft_dm64k.hip's finding
-#ifndef BCFFT_DM256K_PRIO
-#define BCFFT_DM256K_PRIO 3
-#endif
-constexpr int PRIO = BCFFT_DM256K_PRIO;
+constexpr int PRIO = 3;
 constexpr int SC2_OFF = CS_OFF + 1024;              // chunk scale exponents [8 tokens]
 constexpr int RR_OFF = SC2_OFF + 64;                // per-token reference exponents [8]
 constexpr int OS2_OFF = RR_OFF + 64;                // the workgroup's 16 inverse weight scales
@@ -1525,9 +1516,6 @@ bool dm256_eligible(int n_in, int b, int xdt, bool yf32) {
 // of 16 blocks, up to MAXG, once its tiles fill the CUs (bcfft::multigroup_pays)
 bool dm256g_taken(int64_t n, int n_in, int n_out) {
   const int groups = (n_out + d256::NOB - 1) / d256::NOB;
-#ifdef BCFFT_NO_DM256G
-  return false;
-#endif
   return n_in == d256::NI && groups >= 3 && groups <= d256::MAXG && multigroup_pays(n, 3);
 }
 

@@ -17,9 +17,6 @@
 #include "bcfft_device.h"
 #include "bcfft_dm_table.h"
 #include "bcfft_dm_common.h"
-#ifndef BCFFT_DM64_TAB_ONCE
-#define BCFFT_DM64_TAB_ONCE 1
-#endif
 
 namespace bcfft {
 
@@ -137,7 +134,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64_kernel(
     int xwb[2];
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) xwb[pr] = 256 * g + 64 * (pr ^ (g & 1)) + 4 * b16;
-#if BCFFT_DM64_TAB_ONCE
     // A = F^T (16 bin-reals x 32 t) fragments, read once for the four quarters (the X stores
     // between quarters kept the compiler from reusing them: 32 -> 8 transposed reads per token)
     f16x8 afr[2][2];
@@ -152,7 +148,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64_kernel(
             (__attribute__((address_space(3))) s16x4*)(lds + trb1 + 16 * (c ^ cx1)));
         afr[pr][mt] = __builtin_bit_cast(f16x8, __builtin_shufflevector(ra, rb, 0, 1, 2, 3, 4, 5, 6, 7));
       }
-#endif
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
       // x of block 16h + b16: t = 8 g + j (unit g) and t + 32 (unit g + 4), j < 8
@@ -194,16 +189,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64_kernel(
       for (int pr = 0; pr < 2; ++pr)
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
-#if BCFFT_DM64_TAB_ONCE
           const f16x8 af = afr[pr][mt];
-#else
-          const int c = 4 * pr + 2 * mt;            // A = F^T (16 bin-reals x 32 t)
-          const s16x4 ra = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(lds + trb0 + 16 * (c ^ cx0)));
-          const s16x4 rb = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(lds + trb1 + 16 * (c ^ cx1)));
-          const f16x8 af = __builtin_bit_cast(f16x8, __builtin_shufflevector(ra, rb, 0, 1, 2, 3, 4, 5, 6, 7));
-#endif
           acc[2 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, pr ? bdh : bah, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         }
       char* xb = slot + 2048 * h;
@@ -412,15 +398,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64_kernel(
     char* other = lds + ((it + 1) & 1) * REGION;
     const int par = it & 1;
     const bool have = m < n_mtiles;
-#ifndef BCFFT_DM64_MIX
-#define BCFFT_DM64_MIX 1
-#endif
-#ifndef BCFFT_DM64_YPRIO
-#define BCFFT_DM64_YPRIO 1
-#endif
     // waves 0-3 run stage 3 and the next tile's x DMA before their stage 1 (bcfft_dm8.hip's mixed
     // order: a memory-heavy and a transform-heavy wave per SIMD, two DMA bursts per phase)
-    if (BCFFT_DM64_MIX && wave < 4 && it > 0 && have) {
+    if (wave < 4 && it > 0 && have) {
       constexpr int NST = GLU ? 2 : 4;              // stage 3's stores
       stage3(other, par ^ 1, m - gstride);
       if (m + gstride < n_mtiles) {
@@ -437,9 +417,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64_kernel(
         // YPRIO: the transform-first (younger) waves issue ahead of their partner's stage 3
         // (bcfft_dm8.hip's finding): 50.3 -> 47.9 us over six interleaved passes
         // (profiles/r05ac_ab_dm64_yprio.log)
-        if (BCFFT_DM64_YPRIO && BCFFT_DM64_MIX) __builtin_amdgcn_s_setprio(BCFFT_DM64_YPRIO);
+        __builtin_amdgcn_s_setprio(1);
         stage1(region, par);
-        if (BCFFT_DM64_YPRIO && BCFFT_DM64_MIX) __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(0);
       }
       if (it > 0) stage3(other, par ^ 1, m - gstride);
       if (m + gstride < n_mtiles) {
@@ -477,12 +457,10 @@ bool dm64_eligible(int n_in, int b, int xdt, bool yf32) { return b == 64 && n_in
 
 void launch_forward_dm64(const void* x, int64_t n, int n_out, const void* spec, const void* bias, int bias_dt,
                          void* y, bool glu, hipStream_t s) {
-#ifndef BCFFT_NO_DM64G
   if (dm64g_eligible(64, 64, BCFFT_BF16, false, n_out, glu) && multigroup_pays(n, glu ? 5 : 4)) {   // x transformed once
     launch_forward_dm64g(x, n, n_out, spec, bias, bias_dt, y, glu, s);
     return;
   }
-#endif
   if (glu) launch_dm64<true, false>(x, n, n_out, spec, nullptr, BCFFT_NONE, y, s);
   else if (bias_dt != BCFFT_NONE) launch_dm64<false, true>(x, n, n_out, spec, bias, bias_dt, y, s);
   else launch_dm64<false, false>(x, n, n_out, spec, bias, bias_dt, y, s);

@@ -29,9 +29,6 @@
 #include "bcfft_device.h"
 #include "bcfft_dm_table.h"
 #include "bcfft_dm_common.h"
-#ifndef BCFFT_DM64_TAB_ONCE
-#define BCFFT_DM64_TAB_ONCE 1
-#endif
 
 namespace bcfft {
 
@@ -151,7 +148,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64g_kernel(
     int xwb[2];
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) xwb[pr] = 256 * g + 64 * (pr ^ (g & 1)) + 4 * b16;
-#if BCFFT_DM64_TAB_ONCE
     // A = F^T (16 bin-reals x 32 t) fragments, read once for the four quarters (the X stores
     // between quarters kept the compiler from reusing them: 32 -> 8 transposed reads per token)
     f16x8 afr[2][2];
@@ -166,7 +162,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64g_kernel(
             (__attribute__((address_space(3))) s16x4*)(lds + trb1 + 16 * (c ^ cx1)));
         afr[pr][mt] = __builtin_bit_cast(f16x8, __builtin_shufflevector(ra, rb, 0, 1, 2, 3, 4, 5, 6, 7));
       }
-#endif
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
       float xq[2][8];
@@ -207,16 +202,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64g_kernel(
       for (int pr = 0; pr < 2; ++pr)
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
-#if BCFFT_DM64_TAB_ONCE
           const f16x8 af = afr[pr][mt];
-#else
-          const int c = 4 * pr + 2 * mt;
-          const s16x4 ra = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(lds + trb0 + 16 * (c ^ cx0)));
-          const s16x4 rb = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(lds + trb1 + 16 * (c ^ cx1)));
-          const f16x8 af = __builtin_bit_cast(f16x8, __builtin_shufflevector(ra, rb, 0, 1, 2, 3, 4, 5, 6, 7));
-#endif
           acc4[2 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, pr ? bdh : bah, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         }
       char* xb = slot + 2048 * h;

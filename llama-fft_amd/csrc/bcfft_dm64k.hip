@@ -17,7 +17,7 @@
 //    w + 8] -> stage 1 (issuing, per token, the x DMA of the next step's chunk into the other
 //    region) | Ba | stage 2 | Bb | [last chunk: Y of the 16 tokens into the chunk's region | Be].
 //  * Stage 1 on raw bf16 x: the 64-point transform as bf16 MFMAs against F 2^-7 in bf16 hi + lo
-//    (round 5; the even / odd fp16 form before it is kept under BCFFT_DM64K_F16S1 for A/B).
+//    (round 5; it replaced an even / odd fp16 form: git history of this file before round 6).
 //  * Numerics: per-(token, 16-block quarter) power-of-two scales from stage 1 with HEAD bits of
 //    headroom; stage 2 aligns each quarter to the token's running reference exponent (an exact
 //    fp16 power of two on the A rows) and scales the accumulator rows down once when a chunk is
@@ -33,14 +33,6 @@
 #include "bcfft_device.h"
 #include "bcfft_dm_table.h"
 #include "bcfft_dm_common.h"
-
-// the even / odd stage 1 (BCFFT_DM64K_F16S1) loads both quarters of a token's chunk before their
-// two wave reductions, which then
-// interleave (bit-identical; 2-3 % faster at N = 1024 and 8192, tools/ab_dm64k.py);
-// -DBCFFT_DM64K_NO_ILP builds the quarter-by-quarter order for A/B
-#ifndef BCFFT_DM64K_NO_ILP
-#define BCFFT_DM64K_ILP
-#endif
 
 namespace bcfft {
 
@@ -62,11 +54,8 @@ constexpr int HEAD = 4;
 // wave priority falling with the work done in stage 1 (1) and stage 2 (2) (s_setprio, 0 = lowest):
 // waves 4-7, younger than their SIMD partners 0-3, lose every age-ordered arbitration and finished
 // both stages ~1.1 k cycles later; with the priority a wave that is behind issues first (117.7 vs
-// 119.6 us at N = 8192, profiles/r05ll_ab_dm64k_prio.log). -DBCFFT_DM64K_PRIO=0 builds without
-#ifndef BCFFT_DM64K_PRIO
-#define BCFFT_DM64K_PRIO 3
-#endif
-constexpr int PRIO = BCFFT_DM64K_PRIO;
+// 119.6 us at N = 8192, profiles/r05ll_ab_dm64k_prio.log)
+constexpr int PRIO = 3;
 // analysis builds only (results are WRONG when set): 1 no B loads, 2 no stage-1 arithmetic, 4 no
 // stage-2 MFMAs, 8 no stage 3, 16 no x DMA, 32 no y stores
 #ifdef BCFFT_DM64K_ABL
@@ -123,10 +112,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
   const int64_t n_mtiles = (n_tokens + TT - 1) / TT;
   const int gstride = gm.stride;
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
-#ifdef BCFFT_STAMPS
   ANALYSIS_INIT;
-  (void)ablate_flags_;
-#endif
 
   // ---- chunk c of token w + 8 t2 of M-tile m -> its slot by LDS-DMA: piece q = rows 8q +
   // (lane >> 3) of 128 B, unit u of row r at u ^ (r & 7); the buffer range ends at the row end, so
@@ -208,7 +194,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
   // against ~100 for unpack / scale / a, d / rounding; 16 MFMAs instead of 4, issued as soon as
   // x is read (the max reduction runs under them). Products of x below ~2^-110 fall into fp32's
   // subnormal range, as in the reference's fp32 rfft.
-#ifndef BCFFT_DM64K_F16S1
   auto stage1 = [&](char* region, auto&& dma) {
     if constexpr ((ABL & 2) != 0) {
       if (lane < 2) { wsc[wave * 2 + lane] = 0; wsc[(wave + 8) * 2 + lane] = 0; }
@@ -293,136 +278,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
       if constexpr ((PRIO & 1) != 0) __builtin_amdgcn_s_setprio(1);
     }
   };
-#else
-  // the even / odd form (bcfft_dm64.hip's stage 1: a = x_t + x_{t+32}, d = x_t - x_{t+32} scaled
-  // and rounded to fp16, F 2^-7 as one fp16 term), kept for A/B
-  auto stage1 = [&](char* region, auto&& dma) {
-    if constexpr ((ABL & 2) != 0) {
-      if (lane < 2) { wsc[wave * 2 + lane] = 0; wsc[(wave + 8) * 2 + lane] = 0; }
-      dma(0);
-      dma(1);
-      return;
-    }
-    const int l = opaque(lane);
-    const int b16 = l & 15, g = l >> 4;
-    const int q4 = (l & 15) >> 2, p4 = l & 3;
-    const int r0 = 8 * g + q4, r1 = r0 + 4;
-    const int trb0 = F_OFF + 128 * r0 + 8 * (p4 & 1), trb1 = F_OFF + 128 * r1 + 8 * (p4 & 1);
-    const int cx0 = (p4 >> 1) ^ fsw64(r0), cx1 = (p4 >> 1) ^ fsw64(r1);
-    int xwb[2];
-#pragma unroll
-    for (int pr = 0; pr < 2; ++pr) xwb[pr] = 256 * g + 64 * (pr ^ (g & 1)) + 4 * b16;
-#pragma unroll 1
-    for (int t2 = 0; t2 < 2; ++t2) {
-      const int tl = wave + 8 * t2;
-      char* slot = region + tl * XSLOT;
-      dma(t2);
-#ifdef BCFFT_DM64K_ILP
-      // both quarters' x and maxima first, so their two wave reductions (DPP + readlane chains)
-      // can interleave; the per-quarter scales, and so every result, are unchanged
-      float xq2[KC][2][8];
-      int sxq[KC];
-#pragma unroll
-      for (int h = 0; h < KC; ++h) {
-        const char* rowp = slot + (16 * h + b16) * (B * ES);
-#pragma unroll
-        for (int pt = 0; pt < 2; ++pt) {
-          const uint4 w = *reinterpret_cast<const uint4*>(rowp + 16 * ((g + 4 * pt) ^ (b16 & 7)));
-          const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float2 f = unpack16<XT>(ww[e]);
-            xq2[h][pt][2 * e] = f.x;
-            xq2[h][pt][2 * e + 1] = f.y;
-          }
-        }
-      }
-      uint32_t mq[KC];
-#pragma unroll
-      for (int h = 0; h < KC; ++h) {
-        float m0 = 0.f, m1 = 0.f;
-#pragma unroll
-        for (int pt = 0; pt < 2; ++pt)
-#pragma unroll
-          for (int j = 0; j < 8; j += 4) {
-            m0 = amax3(m0, xq2[h][pt][j], xq2[h][pt][j + 1]);
-            m1 = amax3(m1, xq2[h][pt][j + 2], xq2[h][pt][j + 3]);
-          }
-        mq[h] = __float_as_uint(__builtin_fmaxf(m0, m1));
-      }
-#pragma unroll
-      for (int h = 0; h < KC; ++h) mq[h] = wave_umax(mq[h]);
-#pragma unroll
-      for (int h = 0; h < KC; ++h) {
-        sxq[h] = stat_scale_exp(2.f * __uint_as_float(mq[h])) - HEAD;
-        if (l == 0) wsc[tl * 2 + h] = sxq[h] - 7;  // X = D 2^-(sx - 7): the table's 2^-7
-      }
-#endif
-#pragma unroll
-      for (int h = 0; h < KC; ++h) {
-#ifdef BCFFT_DM64K_ILP
-        float (&xq)[2][8] = xq2[h];
-        const int sx = sxq[h];
-#else
-        float xq[2][8];
-        const char* rowp = slot + (16 * h + b16) * (B * ES);
-#pragma unroll
-        for (int pt = 0; pt < 2; ++pt) {
-          const uint4 w = *reinterpret_cast<const uint4*>(rowp + 16 * ((g + 4 * pt) ^ (b16 & 7)));
-          const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float2 f = unpack16<XT>(ww[e]);
-            xq[pt][2 * e] = f.x;
-            xq[pt][2 * e + 1] = f.y;
-          }
-        }
-        float m0 = 0.f, m1 = 0.f;
-#pragma unroll
-        for (int pt = 0; pt < 2; ++pt)
-#pragma unroll
-          for (int j = 0; j < 8; j += 4) {
-            m0 = amax3(m0, xq[pt][j], xq[pt][j + 1]);
-            m1 = amax3(m1, xq[pt][j + 2], xq[pt][j + 3]);
-          }
-        const float mxf = __builtin_fmaxf(m0, m1);
-        const int sx = stat_scale_exp(2.f * __uint_as_float(wave_umax(__float_as_uint(mxf)))) - HEAD;
-        if (l == 0) wsc[tl * 2 + h] = sx - 7;      // X = D 2^-(sx - 7): the table's 2^-7
-#endif
-        const float S = __int_as_float((sx + 127) << 23);
-        uint32_t ah[4], dh[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float u0 = xq[1][2 * e] * S, u1 = xq[1][2 * e + 1] * S;
-          ah[e] = pk_rne(fmaf(xq[0][2 * e], S, u0), fmaf(xq[0][2 * e + 1], S, u1));
-          dh[e] = pk_rne(fmaf(xq[0][2 * e], S, -u0), fmaf(xq[0][2 * e + 1], S, -u1));
-        }
-        const f16x8 bah = frag(ah[0], ah[1], ah[2], ah[3]), bdh = frag(dh[0], dh[1], dh[2], dh[3]);
-        f32x4 acc4[4];
-#pragma unroll
-        for (int pr = 0; pr < 2; ++pr)
-#pragma unroll
-          for (int mt = 0; mt < 2; ++mt) {
-            const int c = 4 * pr + 2 * mt;
-            const s16x4 ra = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) s16x4*)(lds + trb0 + 16 * (c ^ cx0)));
-            const s16x4 rb = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) s16x4*)(lds + trb1 + 16 * (c ^ cx1)));
-            const f16x8 af = __builtin_bit_cast(f16x8, __builtin_shufflevector(ra, rb, 0, 1, 2, 3, 4, 5, 6, 7));
-            acc4[2 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, pr ? bdh : bah, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          }
-        char* xb = slot + 2048 * h;
-#pragma unroll
-        for (int pr = 0; pr < 2; ++pr)
-#pragma unroll
-          for (int mt = 0; mt < 2; ++mt) {
-            *reinterpret_cast<uint32_t*>(xb + xwb[pr] + 1024 * mt) = pk_rne(acc4[2 * pr + mt][0], acc4[2 * pr + mt][1]);
-            *reinterpret_cast<uint32_t*>(xb + xwb[pr] + 1024 * mt + 128) = pk_rne(acc4[2 * pr + mt][2], acc4[2 * pr + mt][3]);
-          }
-      }
-    }
-  };
-#endif
 
   // accumulators [bin of the wave][M-tile][N-tile]: rows 4 yt + r = token 8 mt + 2 yt + (r >> 1),
   // re / im r & 1; reference exponents of the A-row tokens and the accumulator-row tokens
@@ -779,9 +634,4 @@ void launch_forward_dm64k(const void* x, int64_t n, int n_in, int n_out, const v
 
 }  // namespace bcfft
 
-#ifdef BCFFT_STAMPS
-extern "C" int bcfft_set_stamps_dm64k(void* buf) {
-  unsigned long long* p = (unsigned long long*)buf;
-  return hipMemcpyToSymbol(HIP_SYMBOL(bcfft::g_stamps), &p, sizeof(p)) == hipSuccess ? 0 : BCFFT_ERR_HIP;
-}
-#endif
+BCFFT_STAMPS_SETTER(dm64k)

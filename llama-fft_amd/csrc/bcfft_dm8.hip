@@ -77,10 +77,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
   const int64_t n_mtiles = (n_tokens + TT - 1) / TT;
   const int gstride = gm.stride;
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
-#ifdef BCFFT_STAMPS
   ANALYSIS_INIT;
-  (void)ablate_flags_;
-#endif
 
   // ---- x of token `wave` of M-tile m -> its slot by LDS-DMA (the buffer range zero-fills
   // tokens past n_tokens); piece q = rows 4q + (lane >> 4), 256 B each, with the slot's unit
@@ -160,57 +157,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
     int xwb[2];
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) xwb[pr] = 256 * g + 64 * (pr ^ (g & 1)) + 4 * b16;
-#ifdef BCFFT_S1_ILP
-    // both halves' x (packed) and maxima first, so their two wave reductions interleave; the
-    // per-half scales, and so every result, are unchanged
-    uint4 rawx[2][2][2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int pt = 0; pt < 2; ++pt)
-          rawx[h][ks][pt] = *reinterpret_cast<const uint4*>(slot + (16 * h + b16) * (B * ES) + 16 * ((4 * ks + g + 8 * pt) ^ b16));
-    uint32_t mxq[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      float m0f = 0.f, m1f = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int pt = 0; pt < 2; ++pt) {
-          const uint4 w = rawx[h][ks][pt];
-          const float2 f0 = unpack16<XT>(w.x), f1 = unpack16<XT>(w.y), f2 = unpack16<XT>(w.z), f3 = unpack16<XT>(w.w);
-          m0f = amax3(m0f, f0.x, f0.y);
-          m1f = amax3(m1f, f1.x, f1.y);
-          m0f = amax3(m0f, f2.x, f2.y);
-          m1f = amax3(m1f, f3.x, f3.y);
-        }
-      mxq[h] = __float_as_uint(__builtin_fmaxf(m0f, m1f));
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) mxq[h] = wave_umax(mxq[h]);
-#endif
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#ifdef BCFFT_S1_ILP
-      float xv8[2][2][8];
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int pt = 0; pt < 2; ++pt) {
-          const uint4 w = rawx[h][ks][pt];
-          const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float2 f = unpack16<XT>(ww[e]);
-            xv8[ks][pt][2 * e] = f.x;
-            xv8[ks][pt][2 * e + 1] = f.y;
-          }
-        }
-      const int sx = stat_scale_exp(2.f * __uint_as_float(mxq[h]));
-      if (l == 0) wsc[par * 16 + sl * 2 + h] = sx - 7;
-#else
       if (xwait) {
         if (h == 0) wait_vmcnt<NDMA / 2 + XOFF>();
         else wait_vmcnt<XOFF>();
@@ -246,7 +194,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
       const float mxf = __builtin_fmaxf(m0, m1);
       const int sx = stat_scale_exp(2.f * __uint_as_float(wave_umax(__float_as_uint(mxf))));   // |a|, |d| <= 2 max|x|
       if (l == 0) wsc[par * 16 + sl * 2 + h] = sx - 7;      // X = D 2^-(sx - 7): the table's 2^-7
-#endif
       const float S = __int_as_float((sx + 127) << 23);
       f32x4 acc[8];
 #pragma unroll
@@ -510,50 +457,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
     const bool have = m < n_mtiles;
     const int sb = 1 + 6 * (it < 9 ? it : 9);       // stamp slots: iterations 0-8, then the latest
     STAMP(sb);
-#ifdef BCFFT_DM8_FI
-    // F waves 0-3: stage 1 of tokens w and w + 4; I waves 4-7: stage 3 of tokens w - 4 and w of
-    // the previous tile (each SIMD then mixes one F and one I wave); the F waves stream the next
-    // tile's x for their two slots after Ba (the I waves' staging reads of those slots are done)
-    // The pipeline's fill (no stage 3) and drain (no stage 1) keep one token per wave, so that
-    // no wave idles through them.
-    const bool fwave = wave < 4;
-    if (it == 0) {                                  // fill: token w (x streamed by wave w)
-      if (have) {
-        wait_vmcnt<0>();
-        stage1(region, par, wave, false, std::integral_constant<int, 0>{});
-      }
-    } else if (!have) {                             // drain: token w of the last tile
-      stage3(other, par ^ 1, m - gstride, wave);
-    } else if (fwave) {
-      wait_vmcnt<0>();                              // this wave's own x DMA (both slots)
-      STAMP(sb + 1);
-      stage1(region, par, wave, false, std::integral_constant<int, 0>{});
-      stage1(region, par, wave + 4, false, std::integral_constant<int, 0>{});
-    } else {
-      stage3(other, par ^ 1, m - gstride, wave - 4);
-      stage3(other, par ^ 1, m - gstride, wave);
-    }
-    STAMP(sb + 2);
-    STAMP(sb + 3);
-    if (!have) break;
-    lds_barrier();                                  // Ba: X units and scales complete
-    STAMP(sb + 4);
-    if (fwave && m + gstride < n_mtiles) {
-      dma_token(m + gstride, other, wave);
-      dma_token(m + gstride, other, wave + 4);
-    }
-    stage2(region, par);
-#else
-#ifndef BCFFT_DM8_MIX
-#define BCFFT_DM8_MIX 1
-#endif
-#ifndef BCFFT_DM8_YPRIO
-#define BCFFT_DM8_YPRIO 1
-#endif
     // waves 0-3 run stage 3 and the next tile's x DMA before their stage 1, waves 4-7 after it:
     // each SIMD then pairs a memory-heavy wave with a transform-heavy one, and the 64 DMA pieces
     // of the CU issue in two bursts half a phase apart instead of one
-    if (BCFFT_DM8_MIX && wave < 4 && it > 0 && have) {
+    if (wave < 4 && it > 0 && have) {
       STAMP(sb + 1);
       stage3(other, par ^ 1, m - gstride, wave);
       STAMP(sb + 2);
@@ -566,20 +473,14 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
       }
     } else {
       if (have) {
-#if defined(BCFFT_S1_ILP) || (defined(BCFFT_DM8_XWAIT) && BCFFT_DM8_XWAIT == 0)
-        wait_vmcnt<0>();                              // this wave's x (and its older y stores)
-        STAMP(sb + 1);
-        stage1(region, par, wave, false, std::integral_constant<int, 0>{});
-#else
         STAMP(sb + 1);
         // YPRIO: the transform-first waves (the younger of each SIMD pair) issue ahead of their
         // partner's stage 3: their stage 1 was the tile's critical path (6.1 k cycles against 2.6 k,
         // profiles/r05f4_timeline_dm8.txt); with it both waves finish at ~8.1 k and the kernel
         // reads 36.3 -> 35.9 us (profiles/r05ab_ab_dm8_yprio.log)
-        if (BCFFT_DM8_YPRIO && BCFFT_DM8_MIX) __builtin_amdgcn_s_setprio(BCFFT_DM8_YPRIO);
+        __builtin_amdgcn_s_setprio(1);
         stage1(region, par, wave, true, std::integral_constant<int, 0>{});   // waits per half for this wave's x (and its older y stores)
-        if (BCFFT_DM8_YPRIO && BCFFT_DM8_MIX) __builtin_amdgcn_s_setprio(0);
-#endif
+        __builtin_amdgcn_s_setprio(0);
       }
       STAMP(sb + 2);
       if (it > 0) stage3(other, par ^ 1, m - gstride, wave);
@@ -593,7 +494,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
     lds_barrier();                                  // Ba: X units and scales complete
     STAMP(sb + 4);
     stage2(region, par);
-#endif
     lds_barrier();                                  // Bb: Y units complete
     STAMP(sb + 5);
   }
@@ -629,12 +529,7 @@ void launch_forward_dm8(const void* x, int64_t n, int n_out, const void* spec, c
 }
 }  // namespace bcfft
 
-#ifdef BCFFT_STAMPS
 // analysis build only: stamp buffer of bc_forward_dm8_kernel (this TU's copy). Slots per wave: 0
 // start | per iteration it < 9 (base 1 + 6 it, then the latest): +0 top, +1 own x landed, +2
 // stage 1 done, +3 stage 3 + DMA issued, +4 after Ba, +5 stage 2 + Bb done | 63 end
-extern "C" int bcfft_set_stamps_dm8(void* buf) {
-  unsigned long long* p = (unsigned long long*)buf;
-  return hipMemcpyToSymbol(HIP_SYMBOL(bcfft::g_stamps), &p, sizeof(p)) == hipSuccess ? 0 : BCFFT_ERR_HIP;
-}
-#endif
+BCFFT_STAMPS_SETTER(dm8)

@@ -92,10 +92,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmg_kernel(
   const int64_t n_mtiles = (n_tokens + TT - 1) / TT;
   const int64_t gstride = gridDim.x;
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
-#ifdef BCFFT_STAMPS
   ANALYSIS_INIT;
-  (void)ablate_flags_;
-#endif
   const uint4* bimg = reinterpret_cast<const uint4*>(stat + 4);
 
   // ---- x of token `wave` of M-tile m -> its slot by LDS-DMA (bcfft_dm8.hip's: the buffer range
@@ -178,57 +175,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmg_kernel(
     int xwb[2];
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) xwb[pr] = 256 * g + 64 * (pr ^ (g & 1)) + 4 * b16;
-#ifdef BCFFT_S1_ILP
-    // both halves' x (packed) and maxima first, so their two wave reductions interleave; the
-    // per-half scales, and so every result, are unchanged
-    uint4 rawx[2][2][2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int pt = 0; pt < 2; ++pt)
-          rawx[h][ks][pt] = *reinterpret_cast<const uint4*>(slot + (16 * h + b16) * (B * ES) + 16 * ((4 * ks + g + 8 * pt) ^ b16));
-    uint32_t mxq[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      float m0f = 0.f, m1f = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int pt = 0; pt < 2; ++pt) {
-          const uint4 w = rawx[h][ks][pt];
-          const float2 f0 = unpack16<XT>(w.x), f1 = unpack16<XT>(w.y), f2 = unpack16<XT>(w.z), f3 = unpack16<XT>(w.w);
-          m0f = amax3(m0f, f0.x, f0.y);
-          m1f = amax3(m1f, f1.x, f1.y);
-          m0f = amax3(m0f, f2.x, f2.y);
-          m1f = amax3(m1f, f3.x, f3.y);
-        }
-      mxq[h] = __float_as_uint(__builtin_fmaxf(m0f, m1f));
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) mxq[h] = wave_umax(mxq[h]);
-#endif
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#ifdef BCFFT_S1_ILP
-      float xv8[2][2][8];
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int pt = 0; pt < 2; ++pt) {
-          const uint4 w = rawx[h][ks][pt];
-          const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float2 f = unpack16<XT>(ww[e]);
-            xv8[ks][pt][2 * e] = f.x;
-            xv8[ks][pt][2 * e + 1] = f.y;
-          }
-        }
-      const int sx = stat_scale_exp(2.f * __uint_as_float(mxq[h]));
-      if (l == 0) wsc[par * 16 + wave * 2 + h] = sx - 7;
-#else
       float xv8[2][2][8];
       const char* rowp = slot + (16 * h + b16) * (B * ES);
 #pragma unroll
@@ -258,7 +206,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmg_kernel(
       const float mxf = __builtin_fmaxf(m0f, m1f);
       const int sx = stat_scale_exp(2.f * __uint_as_float(wave_umax(__float_as_uint(mxf))));   // |a|, |d| <= 2 max|x|
       if (l == 0) wsc[par * 16 + wave * 2 + h] = sx - 7;    // X = D 2^-(sx - 7): the table's 2^-7
-#endif
       const float S = __int_as_float((sx + 127) << 23);
       f32x4 acc[8];
 #pragma unroll
@@ -604,9 +551,4 @@ void launch_forward_dmg(const void* x, int64_t n, int n_out, const void* spec, c
 }
 }  // namespace bcfft
 
-#ifdef BCFFT_STAMPS
-extern "C" int bcfft_set_stamps_dmg(void* buf) {
-  unsigned long long* p = (unsigned long long*)buf;
-  return hipMemcpyToSymbol(HIP_SYMBOL(bcfft::g_stamps), &p, sizeof(p)) == hipSuccess ? 0 : BCFFT_ERR_HIP;
-}
-#endif
+BCFFT_STAMPS_SETTER(dmg)

@@ -54,10 +54,7 @@ constexpr int ABL = BCFFT_DMK_ABL;
 constexpr int ABL = 0;
 #endif
 // wave priority falling through stage 1 (1) and stage 2 (2): set_prio, bcfft_dm64k.hip's finding
-#ifndef BCFFT_DMK_PRIO
-#define BCFFT_DMK_PRIO 3
-#endif
-constexpr int PRIO = BCFFT_DMK_PRIO;
+constexpr int PRIO = 3;
 
 constexpr int B = 128, NW = 8, BPW = 8, NT = 2, NOG = 32;
 constexpr int XSLOT = 4096 + 64;                    // one token's 16-block x chunk -> X units
@@ -137,10 +134,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dmk_kernel(
   }
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
   const uint4* bimg = reinterpret_cast<const uint4*>(stat + 4);
-#ifdef BCFFT_STAMPS
   ANALYSIS_INIT;
-  (void)ablate_flags_;
-#endif
 
   // ---- x chunk c of token `wave` of M-tile m -> their slots by LDS-DMA. The
   // buffer range ends at the token's row end (a partial last chunk reads zeros) and is empty
@@ -745,13 +739,9 @@ void launch_forward_dmk(const void* x, int64_t n, int n_in, int n_out, const voi
   // halve the weight stream per token). The smaller makespan wins; this model picks the faster
   // size at every measured N (profiles/r02_ab_dmk_tile_switch.log: 16 at N = 3000 and 4096, 8
   // at 5000 and 6144, 16 at 8192, 8 at 1700).
-#ifdef BCFFT_DMK_TILE
-  const bool t16 = BCFFT_DMK_TILE == 16;           // analysis builds: force a tile size
-#else
   const int64_t waves8 = (groups * ((n + 7) / 8) + cus - 1) / cus;
   const int64_t waves16 = (groups * ((n + 15) / 16) + cus - 1) / cus;
   const bool t16 = waves16 * 40 < waves8 * 22;
-#endif
   const int64_t n_mtiles = t16 ? (n + 15) / 16 : (n + 7) / 8;
   const int64_t total = group_grid(cus, groups, n_mtiles);
   const bool hb = bias_dt != BCFFT_NONE;
@@ -835,14 +825,9 @@ void launch_dmk_image(int n_out, int n_in, void* spec, hipStream_t s) {
 
 }  // namespace bcfft
 
-#ifdef BCFFT_STAMPS
 // analysis build only: stamp buffer of bc_forward_dmk_kernel (this TU's copy). Slots per wave: 0
 // start | per tile t < 2 (base 1 + 30 t): +0 step 0 top, +1 stage 3 done, +2 after B0, +3 stage 1
 // done, +4 after Ba, +5 stage 2 done, +6 after Bb; step c in 1..5: +7 + 3 (c - 1) stage 1 done,
 // +8 ... after Ba, +9 ... after Bb | 16-token tiles: +22 after Bc, +23 stage 3 done, +24 after Bd |
 // +25 after Be | 63 end (tools/timeline_dmk.py)
-extern "C" int bcfft_set_stamps_dmk(void* buf) {
-  unsigned long long* p = (unsigned long long*)buf;
-  return hipMemcpyToSymbol(HIP_SYMBOL(bcfft::g_stamps), &p, sizeof(p)) == hipSuccess ? 0 : BCFFT_ERR_HIP;
-}
-#endif
+BCFFT_STAMPS_SETTER(dmk)

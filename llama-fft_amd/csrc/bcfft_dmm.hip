@@ -48,10 +48,7 @@ namespace bcfft {
 namespace dmm {
 // wave priority falling through gate/up stage 2 (1), down stage 2 (2), gate/up stage 3 and
 // down stage 1 (4): set_prio
-#ifndef BCFFT_DMM_PRIO
-#define BCFFT_DMM_PRIO 7
-#endif
-constexpr int PRIO = BCFFT_DMM_PRIO;
+constexpr int PRIO = 7;
 using namespace dmh;
 constexpr int B = 128, NI = 32, KS = 2, NOG = 32, TT = 8, NW = 8;
 constexpr int BW = 8, NT = 2;                       // bins per wave, 16-wide N-tiles

@@ -637,7 +637,7 @@ int ksplit_rows(int64_t rows, int n_chunks, int slots, int min_chunks) {
   return (int)((n_chunks + cps - 1) / cps);
 }
 int mfma_ksplit(int64_t n, int n_in, int b) {
-  if (b > BCFFT_MFMA_MAXB || n <= 0) return 1;
+  if (b > bcfft::BCFFT_MFMA_MAXB || n <= 0) return 1;
   // one chunk per slice pays at decode sizes (<= 4 rows: 24.0 vs 27.7 us at N = 20), two above
   // (35.1 vs 37.3 us at N = 256)
   const int64_t rows = (n + 7) / 8;
@@ -663,7 +663,7 @@ void launch_finish(const float* ws, int kz, int64_t n, int64_t m, const void* bi
 template <int B, int XT, bool YF32>
 void launch_forward(int algo, const void* x, int64_t n, int n_in, int n_out, const void* spec,
                     const void* bias, int bias_dt, void* y, float* ws, hipStream_t s) {
-  if constexpr (B <= BCFFT_MFMA_MAXB) {
+  if constexpr (B <= bcfft::BCFFT_MFMA_MAXB) {
     if (algo == BCFFT_ALGO_MFMA) {
       using G = bcfft::GeoM<B>;
       const int kz = ws ? mfma_ksplit(n, n_in, B) : 1;
@@ -705,7 +705,7 @@ void launch_spectra(const void* c, int c_dt, int n_out, int n_in, int tc, float2
   const unsigned threads = (B / 2) < 64 ? 64u : (unsigned)(B / 2);
   hipLaunchKernelGGL(bcfft::bc_spectra_kernel<B>, dim3(nblk), dim3(threads), 0, s, c, c_dt,
                      n_out, n_in, tc, out);
-  if constexpr (B <= BCFFT_MFMA_MAXB) {
+  if constexpr (B <= bcfft::BCFFT_MFMA_MAXB) {
     const bcfft::SpecLayout sl = bcfft::spec_layout(n_out, n_in, B);
     const int64_t total = sl.img_u32 / 2;
     const unsigned blocks = (unsigned)((total + 255) / 256 < 65535 ? (total + 255) / 256 : 65535);
@@ -775,15 +775,13 @@ static int resolve_algo(int algo, int n_in, int block_size, int xdt = -2, bool y
     return BCFFT_ALGO_SHORT;
   if (bcfft::dm_eligible(n_in, block_size)) return yf32 ? BCFFT_ALGO_DFTX : BCFFT_ALGO_DFT;
   if (bcfft::dm64_eligible(n_in, block_size, xdt, yf32)) return BCFFT_ALGO_DFT;
-#ifndef BCFFT_NO_DM256
   if (bcfft::dm256_eligible(n_in, block_size, xdt, yf32)) return BCFFT_ALGO_DFT;
-#endif
   // K > 4096 at b = 64 (bf16): the streamed-weight DFT kernel once its 16-token tiles fill a few
   // CUs (N = 64: 36.9 us vs the split-K MFMA kernel's 31.4; N = 1024: 39.5 vs 71.9)
-  if (bcfft::dm64k_eligible(n_in, block_size, xdt, yf32) && n_tokens >= BCFFT_DM64K_MIN_TOKENS) return BCFFT_ALGO_DFT;
+  if (bcfft::dm64k_eligible(n_in, block_size, xdt, yf32) && n_tokens >= bcfft::BCFFT_DM64K_MIN_TOKENS) return BCFFT_ALGO_DFT;
   // K > 4096 at b = 128 (bf16): the streamed-weight DFT kernel, from one token up (it beats the
   // split-K MFMA kernel at every measured N: 20.9 vs 23.4 us at N = 1, profiles/r02_dmk_decode_sizes.log)
-  if (bcfft::dmk_eligible(n_in, block_size, xdt, yf32) && n_tokens >= BCFFT_DMK_MIN_TOKENS) return BCFFT_ALGO_DFT;
+  if (bcfft::dmk_eligible(n_in, block_size, xdt, yf32) && n_tokens >= bcfft::BCFFT_DMK_MIN_TOKENS) return BCFFT_ALGO_DFT;
   return bcfft::stat_eligible(n_in, block_size) ? BCFFT_ALGO_STAT
                                                 : (block_size <= 128 ? BCFFT_ALGO_MFMA : BCFFT_ALGO_VALU);
 }
@@ -805,7 +803,7 @@ static int64_t ws_bytes_for(int64_t n_tokens, int in_features, int out_features,
       a == BCFFT_ALGO_SHORT)
     return 0;
   int kz = 1;
-  if (a == BCFFT_ALGO_MFMA && block_size <= BCFFT_MFMA_MAXB) kz = mfma_ksplit(n_tokens, n_in, block_size);
+  if (a == BCFFT_ALGO_MFMA && block_size <= bcfft::BCFFT_MFMA_MAXB) kz = mfma_ksplit(n_tokens, n_in, block_size);
   else if (a == BCFFT_ALGO_VALU || a == BCFFT_ALGO_MFMA) kz = valu_ksplit(n_tokens, n_in, block_size);
   if (kz < 2) return 0;
   return kz * n_tokens * (int64_t)out_features * (int64_t)sizeof(float);   // one fp32 slab per slice
@@ -944,7 +942,7 @@ static int forward_plan(int64_t n_tokens, int in_features, int out_features, int
                   ? "bc_forward_dmg_kernel" : "bc_forward_dm8_kernel";
   else if (a == BCFFT_ALGO_DFT || a == BCFFT_ALGO_DFTX || a == BCFFT_ALGO_DFTP) *kernel = "bc_forward_dm_kernel";
   else if (a == BCFFT_ALGO_STAT) *kernel = "bc_forward_stat_kernel";
-  else if (a == BCFFT_ALGO_MFMA && block_size <= BCFFT_MFMA_MAXB) *kernel = "bc_forward_mfma_kernel";
+  else if (a == BCFFT_ALGO_MFMA && block_size <= bcfft::BCFFT_MFMA_MAXB) *kernel = "bc_forward_mfma_kernel";
   else *kernel = "bc_forward_valu_kernel";
   return a;
 }
@@ -1115,7 +1113,7 @@ int bcfft_forward(const void* x, int x_dtype, int64_t n_tokens, int in_features,
                             bias, bias_dtype, y, y_dtype, BCFFT_ALGO_AUTO, stream);
 }
 
-#if defined(BCFFT_ABLATE) || defined(BCFFT_STAMPS)
+#ifdef BCFFT_ANALYSIS
 // analysis builds only: phase switches of the MFMA kernel (results are WRONG when set):
 // 1 skip MFMAs, 2 skip B-fragment loads, 4 skip forward FFT math, 8 skip inverse FFT math,
 // 16 skip x DMA

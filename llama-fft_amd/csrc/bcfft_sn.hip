@@ -33,11 +33,6 @@ namespace bcfft {
 namespace sn {
 using namespace dmh;
 constexpr int NW = 8;
-// wave priority falling through stage 2's bins (set_prio; bcfft_dm64k.hip's finding)
-#ifndef BCFFT_SN_PRIO
-#define BCFFT_SN_PRIO 0
-#endif
-constexpr bool SN_PRIO = BCFFT_SN_PRIO != 0;
 
 template <int B, int KS, int TT, int ES>
 struct Geo {
@@ -310,7 +305,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_sn_kernel(
 #pragma unroll
     for (int fb = 0; fb < BW; ++fb) {
       const int f = wave * BW + fb;
-      if constexpr (SN_PRIO) set_prio(3 - 4 * fb / BW);
       uint4 raw[KS];
 #pragma unroll
       for (int c = 0; c < KS; ++c) raw[c] = *reinterpret_cast<const uint4*>(ab + (c * H + f) * 128);
@@ -400,16 +394,11 @@ __global__ __launch_bounds__(512, 2) void bc_forward_sn_kernel(
 
 }  // namespace bcfft
 
-#if defined(BCFFT_ABLATE) || defined(BCFFT_STAMPS)
 // analysis builds only: stamp buffer of bc_forward_sn_kernel (this TU's copy). Slots per wave: 0
 // start | 1 x DMA issued | 2 table + scales written, fragments issued | 3 x and table landed |
 // 4 after the prologue barrier | 5 stage 1 done | 6 after its barrier | 7 stage 2 done | 8 after
 // its barrier | 9 stage 3 + stores issued
-extern "C" int bcfft_set_stamps_sn(void* buf) {
-  unsigned long long* p = (unsigned long long*)buf;
-  return hipMemcpyToSymbol(HIP_SYMBOL(bcfft::g_stamps), &p, sizeof(p)) == hipSuccess ? 0 : BCFFT_ERR_HIP;
-}
-#endif
+BCFFT_STAMPS_SETTER(sn)
 
 namespace {
 template <int B, int KS, int TT, int XT, bool YF32>

@@ -306,11 +306,6 @@ __host__ __device__ inline void stat_sigma(int j, double sg[2]) {
   if (L == 4 && j == 3) { sg[0] = 0; sg[1] = -1; }
 }
 
-#ifdef BCFFT_MARKS
-#define MARK(n) asm volatile(";MARK " #n)
-#else
-#define MARK(n) do {} while (0)
-#endif
 
 
 // x staging swizzle (16-B units of a row) that keeps the forward DPP-group reads conflict-free
@@ -1193,7 +1188,7 @@ void launch_stat_image(int b, int n_out, int n_in, void* spec, hipStream_t s) {
 }
 }  // namespace bcfft
 
-#if defined(BCFFT_ABLATE) || defined(BCFFT_STAMPS)
+#ifdef BCFFT_ANALYSIS
 // analysis builds only: switches / stamp buffer of bc_forward_stat_kernel (this TU's copies).
 // 1 skip MFMAs, 2 skip y stores, 4 skip forward FFT math, 8 skip inverse FFT math, 16 skip x DMA,
 // 32 skip A-fragment LDS reads, 64 skip the A im-row transform
