@@ -11,7 +11,7 @@ for o in "$(dirname "$0")"/../llama-fft_amd/lib/obj/*.o; do
   objcopy -O binary --only-section=.hip_fatbin "$o" "$tmp/fat_$n.bin" || exit 1
   $llvm/clang-offload-bundler --unbundle --type=o --input="$tmp/fat_$n.bin" \
     --targets=hipv4-amdgcn-amd-amdhsa--gfx950 --output="$tmp/dev_$n.o" || exit 1
-  $llvm/llvm-objdump -d --no-show-raw-insn "$tmp/dev_$n.o" | sed -E 's/^ *[0-9a-f]+:\s*//; s/\/\/ [0-9A-F]+://' > "$out/$n.s"
+  $llvm/llvm-objdump -d --no-show-raw-insn "$tmp/dev_$n.o" | tail -n +3 | sed -E 's/^ *[0-9a-f]+:\s*//; s/\/\/ [0-9A-F]+://' > "$out/$n.s"
 done
 rm -rf "$tmp"
 md5sum "$out"/*.s
