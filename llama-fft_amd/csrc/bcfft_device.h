@@ -630,6 +630,7 @@ const char* dm256_kernel_name(int64_t n, int n_in, int n_out);   // the kernel l
 void launch_forward_dm256_glu(const void* x, int64_t n, int n_gate, const void* spec, void* h, hipStream_t s);
 // b = 64, K > 4096 (up to 255 input blocks), bf16 x and bf16 y (bcfft_dm64k.hip)
 bool dm64k_eligible(int n_in, int b, int xdt, bool yf32);
+bool dm64k_pairs(int groups);   // two output groups per workgroup (even group counts)
 constexpr int BCFFT_DM64K_MIN_TOKENS = 128;   // AUTO picks the b = 64 streamed-weight kernel from this many tokens
 void launch_forward_dm64k(const void* x, int64_t n, int n_in, int n_out, const void* spec, const void* bias,
                           int bias_dt, void* y, hipStream_t s);

@@ -130,7 +130,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
   // (not in the precise engine: its residual operands leave no registers for the split paths)
   constexpr bool FILL_SPLIT = LATE_W && ES == 4 && EP == 0;
   constexpr bool DRAIN_SPLIT = !GLU && EP == 0;
-  // (round 4 measured and rejected other x-DMA placements and role splits: DESIGN.md section 8c,
+  // (round 4 measured and rejected other x-DMA placements and role splits: docs/HISTORY.md section 8c,
   // item 8, with their A/B logs; their switches are in the git history of this file)
 
   ANALYSIS_INIT;

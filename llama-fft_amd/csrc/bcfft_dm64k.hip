@@ -39,17 +39,28 @@ namespace bcfft {
 namespace dm64k {
 using namespace dmh;
 
-constexpr int B = 64, NW = 8, TT = 16, MT = 2, BW = 4, NT = 2, KC = 2, NOG = 32;
-constexpr int XSLOT = 4096 + 64;                    // one token's chunk (32 blocks x 128 B)
-constexpr int REGION = TT * XSLOT;
-constexpr int F_OFF = 2 * REGION;                   // DFT table image, 32 rows x 128 B
-constexpr int SC_OFF = F_OFF + 4096;                // scale exponents [16 tokens][2 quarters]
-constexpr int RR_OFF = SC_OFF + 128;                // per-token reference exponents [16]
-constexpr int OS_OFF = RR_OFF + 64;                 // the group's 32 inverse weight scales
-constexpr int TB_OFF = OS_OFF + 128;                // stage 1's bf16 hi + lo A fragments (kDmB64)
-constexpr int LDS_BYTES = TB_OFF + 8192;
-constexpr int FRAGS = BW * KC * NT;                 // B fragments per wave and chunk
-constexpr int NDMA = 2 * 4;                         // 1-KiB x DMA pieces per wave and chunk (2 tokens)
+constexpr int B = 64, NW = 8, BW = 4, NT = 2, KC = 2, NOG = 32;
+// NG output groups per workgroup (the template parameter of the kernel): NG = 1, 16-token tiles
+// (two M-tiles of 8, tokens w and w + 8 per wave); NG = 2, 8-token tiles (one M-tile, token w per
+// wave) whose stage 1 serves both groups' stage 2 and stage 3
+template <int NG> struct Geo {
+  static constexpr int TT = 16 / NG, MT = 2 / NG, TPW = 2 / NG;   // tokens per tile / M-tiles / per wave
+  // token slot: the 32-block x chunk (4 KiB) -> X units -> the NG groups' Y units (4 KiB each, at
+  // 4096 g) -> y staging; the stride stays 64 B off the 256-B bank period
+  static constexpr int XS = NG == 1 ? 4096 + 64 : 8192 + 64;
+  static constexpr int REGION = TT * XS;
+  static constexpr int F_OFF = 2 * REGION;          // DFT table image, 32 rows x 128 B
+  static constexpr int SC_OFF = F_OFF + 4096;       // scale exponents [TT tokens][2 quarters]
+  static constexpr int RR_OFF = SC_OFF + 128;       // per-token reference exponents [TT]
+  static constexpr int OS_OFF = RR_OFF + 64;        // the groups' 32 NG inverse weight scales
+  static constexpr int TB_OFF = OS_OFF + 128 * NG;  // stage 1's bf16 hi + lo A fragments (kDmB64)
+  static constexpr int LDS_BYTES = TB_OFF + 8192;
+  static constexpr int NDMA = TPW * 4;              // 1-KiB x DMA pieces per wave and chunk
+  static constexpr int NST = TPW * NG * 4;          // y stores per wave at a tile's first chunk
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+  static_assert(XS % 256 == 64, "slot stride 64 B off the bank period");
+};
+constexpr int FRAGS = BW * KC * NT;                 // B fragments per wave, chunk and group
 constexpr int HEAD = 4;
 // wave priority falling with the work done in stage 1 (1) and stage 2 (2) (s_setprio, 0 = lowest):
 // waves 4-7, younger than their SIMD partners 0-3, lose every age-ordered arbitration and finished
@@ -63,8 +74,6 @@ constexpr int ABL = BCFFT_DM64K_ABL;
 #else
 constexpr int ABL = 0;
 #endif
-static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
-static_assert(XSLOT % 256 == 64, "slot stride 64 B off the bank period");
 
 __device__ __forceinline__ int fsw64(int t) { return (((t >> 1) & 1) << 1) | (((t >> 3) & 1) << 2); }
 __device__ __forceinline__ int yhalf64(int w, int o, int par) { return 2048 * par + 256 * w + 8 * (o ^ (16 * ((w >> 1) & 1))); }
@@ -88,13 +97,18 @@ __device__ __forceinline__ uint32_t pk_umax(uint32_t m, uint32_t w) {
 
 // HB: a bias is added (the runtime bias_dt then names its dtype); without one the store path is
 // straight-line (a runtime test per stored quad split stage 3 into hundreds of basic blocks)
-template <bool HB>
+// NG: output groups per workgroup (dm64k::Geo); NG = 2 needs an even group count
+template <bool HB, int NG>
 __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
     const void* __restrict__ xv, int64_t n_tokens, int n_in, int n_out, const uint32_t* __restrict__ stat,
     const float* __restrict__ osc, const void* __restrict__ bias, int bias_dt, void* __restrict__ yv) {
   using namespace dm64k;
+  using G = Geo<NG>;
   constexpr int XT = BCFFT_BF16;
   constexpr int ES = 2, ESY = 2;
+  constexpr int TT = G::TT, MT = G::MT, TPW = G::TPW, XS = G::XS, REGION = G::REGION;
+  constexpr int F_OFF = G::F_OFF, SC_OFF = G::SC_OFF, RR_OFF = G::RR_OFF, OS_OFF = G::OS_OFF, TB_OFF = G::TB_OFF;
+  constexpr int LDS_BYTES = G::LDS_BYTES, NDMA = G::NDMA, NST = G::NST;
 
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
   int* wsc = reinterpret_cast<int*>(lds + SC_OFF);
@@ -103,8 +117,8 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n_groups = (n_out + NOG - 1) / NOG;
-  const GroupMap gm = group_map(n_groups);
-  const int grp_o = gm.grp, wg_in_grp = gm.lane;
+  const GroupMap gm = group_map((n_groups + NG - 1) / NG);
+  const int sgrp = gm.grp, wg_in_grp = gm.lane;     // groups NG sgrp .. NG sgrp + NG - 1
   const int64_t KX = (int64_t)n_in * B;
   const int64_t M = (int64_t)n_out * B;
   const int nch = (n_in + 31) / 32;
@@ -122,7 +136,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
     const int tl = wave + 8 * t2;
     if constexpr ((ABL & 16) != 0) {                // keep the VMEM count: 4 empty-range loads
       const __amdgpu_buffer_rsrc_t zr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(xv), 0, 0, 0x00020000);
-      const uint32_t d0 = lds_base + (uint32_t)(region - lds) + tl * XSLOT;
+      const uint32_t d0 = lds_base + (uint32_t)(region - lds) + tl * XS;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         uint32_t keep;
@@ -139,7 +153,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<char*>((const char*)xv) + (ok ? tok * KX * ES + (int64_t)c * 4096 : 0), 0,
         ok ? (int)(KX * ES - (int64_t)c * 4096) : 0, 0x00020000);
-    const uint32_t dst0 = lds_base + (uint32_t)(region - lds) + tl * XSLOT;
+    const uint32_t dst0 = lds_base + (uint32_t)(region - lds) + tl * XS;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       uint32_t keep;
@@ -148,17 +162,28 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
     }
   };
 
-  // ---- B fragments (STAT image group grp_o, wave, piece (fb KS + 2c + j) 2 + nt), asm loads
+  // ---- B fragments (STAT image group NG sgrp + g, wave, piece (fb KS + 2c + j) 2 + nt), asm loads
   // counted by hand (bcfft_dmk.hip's scheme): wait_b is their one wait, with the exact number of
   // younger VMEM operations, and it redefines the registers it waited for
   const int npiece = BW * KS * NT;
-  const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint32_t*>(stat + 4) + ((int64_t)(grp_o * NW + wave) * npiece) * 256, 0, npiece * 1024, 0x00020000);
-  // fragment (fb, j, nt) of chunk c; K-step 2c + 1 past the image (odd KS, last chunk) reads zeros
-  auto load_b1 = [&](int c, int fb, int j, int nt, u32x4 (&breg)[BW][KC][NT], bool live) {
+  __amdgpu_buffer_rsrc_t brs[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g)
+    brs[g] = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t*>(stat + 4) + ((int64_t)((NG * sgrp + g) * NW + wave) * npiece) * 256, 0, npiece * 1024,
+        0x00020000);
+  // fragment (fb, j, nt) of group g, chunk c; K-step 2c + 1 past the image (odd KS, last chunk)
+  // reads zeros
+  auto load_b1 = [&](int g, int c, int fb, int j, int nt, u32x4 (&breg)[BW][KC][NT], bool live) {
     const int ks = 2 * c + j;
     const int vo = opaque(lane) * 16 + (live && ks < KS && (ABL & 1) == 0 ? (fb * KS + ks) * 2 + nt : npiece) * 1024;
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(breg[fb][j][nt]) : "v"(vo), "s"(brs));
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(breg[fb][j][nt]) : "v"(vo), "s"(brs[g]));
+  };
+  // NG = 2: the wait for one bin's four fragments, with the number of younger loads (always 12:
+  // the later bins of the same group, then the next group's fragments of the earlier bins)
+  auto wait_bin = [&](int fb, u32x4 (&breg)[BW][KC][NT]) {
+    asm volatile("s_waitcnt vmcnt(12) ; bcfft-wait %0 %1 %2 %3"
+                 : "+v"(breg[fb][0][0]), "+v"(breg[fb][0][1]), "+v"(breg[fb][1][0]), "+v"(breg[fb][1][1]) :: "memory");
   };
   auto wait_b = [&](auto n_tag, u32x4 (&breg)[BW][KC][NT]) {
     constexpr int N = decltype(n_tag)::value;
@@ -180,7 +205,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
     const int t = tid >> 3, ch = tid & 7;
     *reinterpret_cast<uint4*>(lds + F_OFF + 128 * t + 16 * (ch ^ fsw64(t))) = tab[tid];
   }
-  if (tid < 32) reinterpret_cast<float*>(lds + OS_OFF)[tid] = osc[grp_o * 32 + tid];
+  if (tid < 32 * NG) reinterpret_cast<float*>(lds + OS_OFF)[tid] = osc[NG * sgrp * 32 + tid];
   reinterpret_cast<uint4*>(lds + TB_OFF)[tid] = reinterpret_cast<const uint4*>(kDmB64)[tid];
   wait_vmcnt<0>();
   lds_barrier();
@@ -196,9 +221,11 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
   // subnormal range, as in the reference's fp32 rfft.
   auto stage1 = [&](char* region, auto&& dma) {
     if constexpr ((ABL & 2) != 0) {
-      if (lane < 2) { wsc[wave * 2 + lane] = 0; wsc[(wave + 8) * 2 + lane] = 0; }
-      dma(0);
-      dma(1);
+#pragma unroll
+      for (int t2 = 0; t2 < TPW; ++t2) {
+        if (lane < 2) wsc[(wave + 8 * t2) * 2 + lane] = 0;
+        dma(t2);
+      }
       return;
     }
     const int l = opaque(lane);
@@ -219,9 +246,9 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
         for (int tm = 0; tm < 2; ++tm)
           tab[pr][mt][tm] = *reinterpret_cast<const bf16x8*>(lds + TB_OFF + 2048 * (2 * pr + mt) + 1024 * tm + 16 * l);
 #pragma unroll 1
-    for (int t2 = 0; t2 < 2; ++t2) {
+    for (int t2 = 0; t2 < TPW; ++t2) {
       const int tl = wave + 8 * t2;
-      char* slot = region + tl * XSLOT;
+      char* slot = region + tl * XS;
       uint4 xr[KC][2];
 #pragma unroll
       for (int h = 0; h < KC; ++h)
@@ -281,20 +308,25 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
 
   // accumulators [bin of the wave][M-tile][N-tile]: rows 4 yt + r = token 8 mt + 2 yt + (r >> 1),
   // re / im r & 1; reference exponents of the A-row tokens and the accumulator-row tokens
-  f32x4 acc[BW][MT][NT];
+  f32x4 acc[NG][BW][MT][NT];
 #pragma unroll
-  for (int fb = 0; fb < BW; ++fb)
+  for (int g = 0; g < NG; ++g)
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+    for (int fb = 0; fb < BW; ++fb)
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[fb][mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int ra[MT] = {0, 0};
-  int rc[MT][2] = {{0, 0}, {0, 0}};
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[g][fb][mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int ra[MT], rc[MT][2];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) ra[mt] = rc[mt][0] = rc[mt][1] = 0;
 
-  // ---- stage 2 (all waves): the chunk's per-bin complex MAC on bins 4 wave + fb for the 16
-  // tokens, accumulated; each fragment's successor for the next step (nb >= 0) is loaded into
-  // its registers after its last MFMA. One call site.
-  auto stage2 = [&](char* region, u32x4 (&breg)[BW][KC][NT], int nb, bool first, bool tile0) {
+  // ---- stage 2 (all waves): the chunk's per-bin complex MAC on bins 4 wave + fb for the TT
+  // tokens, accumulated. NG = 1: each fragment's successor for the next step (nb >= 0) is loaded
+  // into its registers after its last MFMA. NG = 2: group 0's fragments are in the registers at
+  // entry; after each group-0 bin its group-1 fragments are loaded into them, and after each
+  // group-1 bin the next step's group-0 ones. One call site.
+  auto stage2 = [&](char* region, u32x4 (&breg)[BW][KC][NT], int c_now, int nb, bool first, bool tile0) {
     const int ml = opaque(lane);
     const int arow = ml & 15, kb = ml >> 4;
     const int a_t = arow >> 1, a_reim = arow & 1;
@@ -333,13 +365,15 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
       }
       if (__builtin_amdgcn_ballot_w64(need)) {
 #pragma unroll
-        for (int fb = 0; fb < BW; ++fb)
+        for (int g = 0; g < NG; ++g)
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
+          for (int fb = 0; fb < BW; ++fb)
 #pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
+            for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-              for (int r = 0; r < 4; ++r) acc[fb][mt][nt][r] *= fct[mt][r >> 1];
+              for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[g][fb][mt][nt][r] *= fct[mt][r >> 1];
       }
     }
     uint32_t amul[MT][KC], amul0[MT][KC];
@@ -358,58 +392,81 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
     // previous tile's stage-3 stores before it. One operand-carrying wait on every path (a wait
     // per branch made the compiler copy the 16 fragments where the paths join)
     if (!tile0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");
-    wait_b(std::integral_constant<int, 8 + NDMA>{}, breg);
+    wait_b(std::integral_constant<int, NST + NDMA>{}, breg);
     const bool more = nb >= 0;
     const int nc = more ? nb : 0;
     // A rows of bin 4 wave + fb: X units of the 8 tokens of M-tile mt, K-step j; the next bin's
     // four units are read while this bin's are scaled and multiplied (LDS latency off the chain)
-    const char* abase = region + a_t * XSLOT + 256 * wave + 16 * kb;
-    auto a_off = [&](int fb, int j, int mt) { return 8 * mt * XSLOT + ((fb & 1) ? -sw : sw) + 64 * fb + 2048 * j; };
-    uint4 araw[2][KC][MT];
-#pragma unroll
-    for (int j = 0; j < KC; ++j)
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) araw[0][j][mt] = *reinterpret_cast<const uint4*>(abase + a_off(0, j, mt));
+    const char* abase = region + a_t * XS + 256 * wave + 16 * kb;
+    auto a_off = [&](int fb, int j, int mt) { return 8 * mt * XS + ((fb & 1) ? -sw : sw) + 64 * fb + 2048 * j; };
     const bool bin0 = wave == 0;                    // bin 0 (wave 0, fb 0): (X_0, X_32), no swap
+    // NG = 2 (one M-tile): group 0's scaled A rows are kept for group 1
+    f16x8 acache[NG == 2 ? BW : 1][KC];
 #pragma unroll
-    for (int fb = 0; fb < BW; ++fb) {
-      if constexpr ((PRIO & 2) != 0) set_prio(3 - fb);
-      if (fb + 1 < BW) {
+    for (int g = 0; g < NG; ++g) {
+      const bool reuse = NG == 2 && g == 1;
+      uint4 araw[2][KC][MT];
+      if (!reuse) {
 #pragma unroll
         for (int j = 0; j < KC; ++j)
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-            araw[(fb + 1) & 1][j][mt] = *reinterpret_cast<const uint4*>(abase + a_off(fb + 1, j, mt));
+          for (int mt = 0; mt < MT; ++mt) araw[0][j][mt] = *reinterpret_cast<const uint4*>(abase + a_off(0, j, mt));
       }
-      const uint32_t sel = (fb == 0 && bin0) ? 0x03020100u : a_sel;
 #pragma unroll
-      for (int j = 0; j < KC; ++j) {
+      for (int fb = 0; fb < BW; ++fb) {
+        if constexpr ((PRIO & 2) != 0) set_prio(3 - (fb + g * BW) * 4 / (NG * BW));
+        if (!reuse && fb + 1 < BW) {
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const uint32_t mul = (fb == 0 && bin0) ? amul0[mt][j] : amul[mt][j];
-          uint4 raw = araw[fb & 1][j][mt];
-          raw.x = pkmul(__builtin_amdgcn_perm(raw.x, raw.x, sel), mul);
-          raw.y = pkmul(__builtin_amdgcn_perm(raw.y, raw.y, sel), mul);
-          raw.z = pkmul(__builtin_amdgcn_perm(raw.z, raw.z, sel), mul);
-          raw.w = pkmul(__builtin_amdgcn_perm(raw.w, raw.w, sel), mul);
-          const f16x8 a = __builtin_bit_cast(f16x8, raw);
+          for (int j = 0; j < KC; ++j)
 #pragma unroll
-          for (int nt = 0; nt < NT; ++nt)
-            if constexpr ((ABL & 4) != 0)
-              acc[fb][mt][nt] += f32x4{a[0], a[1], __builtin_bit_cast(f16x8, breg[fb][j][nt])[0], 0.f};
-            else
-              acc[fb][mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, __builtin_bit_cast(f16x8, breg[fb][j][nt]),
-                                                                       acc[fb][mt][nt], 0, 0, 0);
+            for (int mt = 0; mt < MT; ++mt)
+              araw[(fb + 1) & 1][j][mt] = *reinterpret_cast<const uint4*>(abase + a_off(fb + 1, j, mt));
         }
-        // the next step's fragments; past the last step an empty-range load (no branch, no copy)
-        load_b1(nc, fb, j, 0, breg, more);
-        load_b1(nc, fb, j, 1, breg, more);
+        if (NG == 2 && g == 1) wait_bin(fb, breg);   // this bin's group-1 fragments
+        const uint32_t sel = (fb == 0 && bin0) ? 0x03020100u : a_sel;
+#pragma unroll
+        for (int j = 0; j < KC; ++j) {
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            f16x8 a;
+            if (reuse) {
+              a = acache[fb][j];
+            } else {
+              const uint32_t mul = (fb == 0 && bin0) ? amul0[mt][j] : amul[mt][j];
+              uint4 raw = araw[fb & 1][j][mt];
+              raw.x = pkmul(__builtin_amdgcn_perm(raw.x, raw.x, sel), mul);
+              raw.y = pkmul(__builtin_amdgcn_perm(raw.y, raw.y, sel), mul);
+              raw.z = pkmul(__builtin_amdgcn_perm(raw.z, raw.z, sel), mul);
+              raw.w = pkmul(__builtin_amdgcn_perm(raw.w, raw.w, sel), mul);
+              a = __builtin_bit_cast(f16x8, raw);
+              if (NG == 2) acache[fb][j] = a;
+            }
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+              if constexpr ((ABL & 4) != 0)
+                acc[g][fb][mt][nt] += f32x4{a[0], a[1], __builtin_bit_cast(f16x8, breg[fb][j][nt])[0], 0.f};
+              else
+                acc[g][fb][mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, __builtin_bit_cast(f16x8, breg[fb][j][nt]),
+                                                                            acc[g][fb][mt][nt], 0, 0, 0);
+          }
+          // the next fragments into these registers (NG = 2, group 0: group 1's of this step;
+          // otherwise the next step's group 0); past the last step an empty-range load (no
+          // branch, no copy)
+          if (NG == 2 && g == 0) {
+            load_b1(1, c_now, fb, j, 0, breg, true);
+            load_b1(1, c_now, fb, j, 1, breg, true);
+          } else {
+            load_b1(0, nc, fb, j, 0, breg, more);
+            load_b1(0, nc, fb, j, 1, breg, more);
+          }
+        }
       }
     }
   };
 
-  // ---- Y of the 16 tokens (fp16 half-units, bcfft_dm64.hip's map) into their slots of a
-  // region; the reference exponents into wrr; the accumulators restart at zero
+  // ---- Y of the TT tokens (fp16 half-units, bcfft_dm64.hip's map; group g's at 4096 g of the
+  // slot) into their slots of a region; the reference exponents into wrr; the accumulators
+  // restart at zero
   auto ywrite = [&](char* region) {
     const int ml = opaque(lane);
     const int yt = ml >> 4;
@@ -423,37 +480,42 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
     }
     const int ox = 16 * ((wave >> 1) & 1);
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      uint32_t yh[BW][NT][2];
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        uint32_t yh[BW][NT][2];
+#pragma unroll
+        for (int fb = 0; fb < BW; ++fb)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+              yh[fb][nt][s2] = pk_rne(acc[g][fb][mt][nt][2 * s2] * YS, acc[g][fb][mt][nt][2 * s2 + 1] * YS);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          char* yb = region + (8 * mt + 2 * yt + s2) * XS + 4096 * g + 256 * wave;
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) {         // yhalf64(wave, 16 nt + o16, par)
+            const int oo = 8 * ((16 * nt + (ml & 15)) ^ ox);
+            *reinterpret_cast<uint2*>(yb + oo) = make_uint2(yh[0][nt][s2], yh[2][nt][s2]);
+            *reinterpret_cast<uint2*>(yb + 2048 + oo) = make_uint2(yh[1][nt][s2], yh[3][nt][s2]);
+          }
+        }
+      }
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
 #pragma unroll
       for (int fb = 0; fb < BW; ++fb)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
+        for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2)
-            yh[fb][nt][s2] = pk_rne(acc[fb][mt][nt][2 * s2] * YS, acc[fb][mt][nt][2 * s2 + 1] * YS);
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        char* yb = region + (8 * mt + 2 * yt + s2) * XSLOT + 256 * wave;
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {           // yhalf64(wave, 16 nt + o16, par)
-          const int oo = 8 * ((16 * nt + (ml & 15)) ^ ox);
-          *reinterpret_cast<uint2*>(yb + oo) = make_uint2(yh[0][nt][s2], yh[2][nt][s2]);
-          *reinterpret_cast<uint2*>(yb + 2048 + oo) = make_uint2(yh[1][nt][s2], yh[3][nt][s2]);
-        }
-      }
-    }
-#pragma unroll
-    for (int fb = 0; fb < BW; ++fb)
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[fb][mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int nt = 0; nt < NT; ++nt) acc[g][fb][mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
 
-  // ---- stage 3 (token slot tl of a region, reference exponent rref): bcfft_dm64.hip's stage 3;
-  // tok < 0 stores nothing (the stores are still issued, with an empty range)
-  auto stage3 = [&](char* region, int tl, int rref, int64_t tok) {
+  // ---- stage 3 (token slot tl of a region, group g of the workgroup's, reference exponent rref):
+  // bcfft_dm64.hip's stage 3; tok < 0 stores nothing (the stores are still issued, with an empty
+  // range)
+  auto stage3 = [&](char* region, int tl, int gi, int rref, int64_t tok) {
     if constexpr ((ABL & 8) != 0) {                 // keep the VMEM count: 4 empty-range stores
       const __amdgpu_buffer_rsrc_t zr = __builtin_amdgcn_make_buffer_rsrc(yv, 0, 0, 0x00020000);
 #pragma unroll
@@ -462,10 +524,11 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
     }
     const int l = opaque(lane);
     const int o16 = l & 15, g = l >> 4;
-    char* slot = region + tl * XSLOT;
+    char* slot = region + tl * XS + 4096 * gi;
+    const int grp_o = NG * sgrp + gi;
     float ysc[NT];
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) ysc[nt] = __builtin_ldexpf(reinterpret_cast<const float*>(lds + OS_OFF)[16 * nt + o16], 30 - rref);
+    for (int nt = 0; nt < NT; ++nt) ysc[nt] = __builtin_ldexpf(reinterpret_cast<const float*>(lds + OS_OFF)[32 * gi + 16 * nt + o16], 30 - rref);
     uint4 yf[2][NT];
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr)
@@ -548,14 +611,15 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
   //           stage 2 on B(c) (loaded in the previous step), loading the next step's B      | Bb |
   //   c last  Y of the tile into this region                                                 | Be |
   // VMEM younger than x(m, c) when it is waited for: B(c) 16 (the previous step's stage 2) and,
-  // at c = 0, the 8 stores (the first step's x and B were waited for up front).
+  // at c = 0, the NST stores (the first step's x and B were waited for up front); NG = 2: B(c) is
+  // both groups' fragments (group 1 of this step and group 0 of the next, 2 FRAGS).
   u32x4 breg[BW][KC][NT];
 #pragma unroll
   for (int fb = 0; fb < BW; ++fb)
 #pragma unroll
     for (int j = 0; j < KC; ++j) {
-      load_b1(0, fb, j, 0, breg, true);
-      load_b1(0, fb, j, 1, breg, true);
+      load_b1(0, 0, fb, j, 0, breg, true);
+      load_b1(0, 0, fb, j, 1, breg, true);
     }
   wait_vmcnt<0>();
   int rsel = 0;
@@ -571,8 +635,11 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
     const bool tile0 = c == 0;
     DST(0);
     if (tile0) {
-      stage3(other, wave, wrr[wave], mprev >= 0 ? mprev * TT + wave : -1);
-      stage3(other, wave + 8, wrr[wave + 8], mprev >= 0 ? mprev * TT + wave + 8 : -1);
+#pragma unroll
+      for (int t2 = 0; t2 < TPW; ++t2)
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+          stage3(other, wave + 8 * t2, g, wrr[wave + 8 * t2], mprev >= 0 ? mprev * TT + wave + 8 * t2 : -1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slots' staging reads are done
     }
     DST(1);
@@ -581,14 +648,14 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
     const int cn = last ? 0 : c + 1;
     DST(2);
     // x(m, c) landed: younger VMEM is B(c) (the previous step's stage 2) and, at c = 0, the stores
-    if (tile0) wait_vmcnt<FRAGS + 8>();
-    else wait_vmcnt<FRAGS>();
+    if (tile0) wait_vmcnt<NG * FRAGS + NST>();
+    else wait_vmcnt<NG * FRAGS>();
     DST(3);
     stage1(region, [&](int t2) { dma_tok(mn, cn, other, t2); });
     DST(4);
     lds_barrier();                                  // Ba: X units and quarter scales complete
     DST(5);
-    stage2(region, breg, mn < n_mtiles ? cn : -1, tile0, tile0);
+    stage2(region, breg, c, mn < n_mtiles ? cn : -1, tile0, tile0);
     DST(6);
     lds_barrier();                                  // Bb: every read of this chunk's X done
     DST(7);
@@ -603,14 +670,22 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
     c = cn;
   }
   char* yreg = lds + (rsel ^ 1) * REGION;
-  stage3(yreg, wave, wrr[wave], mprev >= 0 ? mprev * TT + wave : -1);
-  stage3(yreg, wave + 8, wrr[wave + 8], mprev >= 0 ? mprev * TT + wave + 8 : -1);
+#pragma unroll
+  for (int t2 = 0; t2 < TPW; ++t2)
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+      stage3(yreg, wave + 8 * t2, g, wrr[wave + 8 * t2], mprev >= 0 ? mprev * TT + wave + 8 * t2 : -1);
   // the last step's empty-range B loads: waited for with the fragments as operands, so that their
   // registers stay reserved (not reused by ywrite / stage 3) until the loads have returned
   wait_b(std::integral_constant<int, 0>{}, breg);
 }
 
 #undef DST
+
+#ifndef BCFFT_DM64K_PAIRS
+#define BCFFT_DM64K_PAIRS 1
+#endif
+bool dm64k_pairs(int groups) { return BCFFT_DM64K_PAIRS != 0 && groups % 2 == 0; }
 
 bool dm64k_eligible(int n_in, int b, int xdt, bool yf32) {
   return dm64k_geometry(n_in, b) && xdt == BCFFT_BF16 && !yf32;
@@ -620,16 +695,27 @@ void launch_forward_dm64k(const void* x, int64_t n, int n_in, int n_out, const v
                           int bias_dt, void* y, hipStream_t s) {
   const int groups = (n_out + dm64k::NOG - 1) / dm64k::NOG;
   const SpecLayout sl = spec_layout(n_out, n_in, 64);
-  const int64_t n_mtiles = (n + dm64k::TT - 1) / dm64k::TT;
-  const int64_t total = group_grid(device_cu_count(), groups, n_mtiles);
   const uint32_t* stat = reinterpret_cast<const uint32_t*>(spec) + sl.stat_off_u32;
   const float* osc = reinterpret_cast<const float*>(spec) + sl.osc_off_u32;
+  const int cus = device_cu_count();
+  // an even group count: two groups per workgroup (stage 1 once for both)
+  if (dm64k_pairs(groups)) {
+    const int64_t total = group_grid(cus, groups / 2, (n + dm64k::Geo<2>::TT - 1) / dm64k::Geo<2>::TT);
+    if (bias_dt != BCFFT_NONE)
+      hipLaunchKernelGGL((bc_forward_dm64k_kernel<true, 2>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out,
+                         stat, osc, bias, bias_dt, y);
+    else
+      hipLaunchKernelGGL((bc_forward_dm64k_kernel<false, 2>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out,
+                         stat, osc, bias, bias_dt, y);
+    return;
+  }
+  const int64_t total = group_grid(cus, groups, (n + dm64k::Geo<1>::TT - 1) / dm64k::Geo<1>::TT);
   if (bias_dt != BCFFT_NONE)
-    hipLaunchKernelGGL(bc_forward_dm64k_kernel<true>, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat, osc,
-                       bias, bias_dt, y);
+    hipLaunchKernelGGL((bc_forward_dm64k_kernel<true, 1>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out,
+                       stat, osc, bias, bias_dt, y);
   else
-    hipLaunchKernelGGL(bc_forward_dm64k_kernel<false>, dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out, stat,
-                       osc, bias, bias_dt, y);
+    hipLaunchKernelGGL((bc_forward_dm64k_kernel<false, 1>), dim3((unsigned)total), dim3(512), 0, s, x, n, n_in, n_out,
+                       stat, osc, bias, bias_dt, y);
 }
 
 }  // namespace bcfft
