@@ -29,6 +29,9 @@
 // y staging), the 4 KiB DFT table (stage 3), stage 1's 8 KiB bf16 A fragments, the scales.
 #ifndef BCFFT_STREAM_POLICY
 #define BCFFT_STREAM_POLICY 3                       // write-through y stores (level to 1 % faster; nt x loads slower, profiles/r04_ab_stream_policy_split.log)
+// (the two-group workgroups (NG = 2) read x with nt on top, below: each token is read once by one
+// CU, and the fragments of both groups then stay in L2: HBM reads 235 -> 201 MB for 180 MB of x,
+// 116.5 -> 113.8 us at 11008 -> 4096, N = 8192; profiles/r06f_ab_dm64k_pairs_nt.log)
 #endif
 #include "bcfft_device.h"
 #include "bcfft_dm_table.h"
@@ -157,8 +160,12 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm64k_kernel(
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       uint32_t keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen" BCFFT_XPOL " lds\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep) : "v"(vb), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
+      if constexpr (NG == 2)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen nt lds\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(vb), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
+      else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen" BCFFT_XPOL " lds\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(vb), "s"(xrs), "s"(dst0 + q * 1024), "s"(q * 1024) : "memory");
     }
   };
 
