@@ -52,11 +52,12 @@ enum bcfft_dtype { BCFFT_NONE = -1, BCFFT_F32 = 0, BCFFT_F16 = 1, BCFFT_BF16 = 2
  *  DFTX: DFT with the per-bin products also split hi + lo before the inverse transform:
  *        ~2.8e-4 relative and linear in x to ~1e-6, ~6 % slower.
  *  DFTP: the precise engine: DFTX with the rounding residual of every single fp16 term (the DFT
- *        table in both transforms and the weight spectra) added back through fp8 MFMAs into the
- *        same fp32 accumulators: ~1e-5 relative, per token ~1e-5 times its cancellation (the
- *        reference's fp32 arithmetic class). Geometry as DFTX; fp32 x and outputs with no bias
- *        or an fp32 bias (16-bit x, outputs or biases run DFTX, whose error already sits below
- *        the 16-bit rounding the reference applies to the output, patch_llama_fft.py:266).
+ *        table in both transforms and the weight spectra) added back through fp8 MFMAs (in fp32
+ *        accumulators of their own, joined to the fp16 products'): ~2e-5 relative, per token
+ *        ~1e-5 times its cancellation (the reference's fp32 arithmetic class). Geometry as DFTX;
+ *        fp32 outputs: fp32 x with no, an fp32 or a 16-bit bias, 16-bit x with no or an fp32 bias
+ *        (16-bit outputs run DFTX, whose error already sits below the 16-bit rounding the
+ *        reference applies to the output, patch_llama_fft.py:266).
  *  AUTO: at block_size 128 with in_features 4096, DFTX for fp32 outputs (linear in x, which the
  *        fp32 backward's dx relies on) and DFT for 16-bit outputs (whose own rounding dominates);
  *        DFT on its other geometries; else STAT where eligible, else MFMA for block_size <= 128,
@@ -132,8 +133,9 @@ int bcfft_forward_algo(const void* x, int x_dtype, int64_t n_tokens, int in_feat
  * dtypes with the workspace bcfft_forward_workspace_bytes_io asks for; < 0 where it would refuse
  * the call. Host logic: nothing is launched. Replaces nothing in the reference (its forward has one
  * code path); benchmarks and tests use it to name what they time. BCFFT_ALGO_DFTP resolves to
- * BCFFT_ALGO_DFTX unless x and y are both fp32 (the precise engine's only form); a 16-bit bias,
- * which this query does not see, also runs DFTX. */
+ * BCFFT_ALGO_DFTX unless y is fp32 (the precise engine's forms: fp32 x with any bias, 16-bit x with
+ * no or an fp32 bias); a 16-bit bias on 16-bit x with an fp32 y, which this query does not see,
+ * also runs DFTX. */
 int bcfft_forward_resolve(int64_t n_tokens, int in_features, int out_features, int block_size, int algo,
                           int x_dtype, int y_dtype);
 

@@ -582,6 +582,7 @@ inline bool sn_tt2(int64_t n_tokens, int n_out) {
 }
 // DFT-on-MFMA kernel (bcfft_dm.hip): the STAT image's geometry subset b = 128, K = 4096
 bool dm_eligible(int n_in, int b);
+bool dftp_serves(int xdt, bool yf32, int bias_dt);   // the precise engine's I/O forms (bcfft_dm.hip)
 bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, int mode, const void* x, int64_t n, int n_out,
                        const void* spec, const void* bias, int bias_dt, void* y, hipStream_t s);
 bool launch_forward_dm_glu(int b, int n_in, int xdt, int mode, const void* x, int64_t n, int n_gate,

@@ -89,6 +89,15 @@ __device__ __forceinline__ long e4m3x8_s6(uint32_t w0, uint32_t w1, uint32_t w2,
   return (long)(((uint64_t)__builtin_bit_cast(uint32_t, hi) << 32) | __builtin_bit_cast(uint32_t, lo));
 }
 
+// An MFMA that reads as SrcC the result of an MFMA of ANOTHER opcode (here f16 <-> fp8_bf8) issued
+// fewer than ~6 instructions before it reads a stale C on gfx950 (every lane; tools/probe/srcc.hip:
+// wrong at 0-3 independent VALU between them, right at 6, profiles/r06j_mfma_srcc_chain_probe.txt).
+// hipcc forwards same-opcode accumulation chains back to back, correctly, and inserts no wait
+// states for the cross-opcode pair either. xdl_gap sits between the two MFMAs of such a pair: it
+// names the accumulator, so the compiler cannot move either MFMA across it, and its 8 wait states
+// plus the instruction give the distance (tools/mfma_audit.py checks every kernel for the pair).
+__device__ __forceinline__ void xdl_gap(f32x4& acc) { asm volatile("s_nop 7" : "+v"(acc)); }
+
 // EP (precise engine, BCFFT_ALGO_DFTP; bit 1: stage-1 table residual, 2: weight residual, 4:
 // stage-3 table residual; 0 = the dft / dftx kernel): every fp16 single term of the dftx kernel
 // gets its rounding residual back through an fp8 MFMA into the same fp32 accumulator:
@@ -382,8 +391,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
             }
             if constexpr ((EP & 1) != 0) {          // + e4m3 table residual x bf8(hi), pair-rows 16 ks + 4 g + q
               const s16x4 rl = rlv[4 * pr + mt];
+              xdl_gap(acc[4 * pr + mt]);             // f16 -> fp8 on one accumulator (xdl_gap)
               acc[4 * pr + mt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_bf8(__builtin_bit_cast(long, rl), pr ? b8d : b8a,
                                                                            acc[4 * pr + mt], 0, 0, 0);
+              xdl_gap(acc[4 * pr + mt]);             // ... and on to the next K-step's f16 MFMAs
             }
           }
       }
@@ -628,6 +639,13 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
             O[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gcur[ks][1], __builtin_bit_cast(f16x8, yf[yp][ks][1][nt]), O[nt], 0, 0, 0);
           }
       if constexpr ((EP & 4) != 0) {                // + e4m3 table residual x bf8(Y hi)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {           // f16 -> fp8 on one accumulator (xdl_gap)
+          if ((ntm >> nt) & 1) {
+            xdl_gap(E[nt]);
+            xdl_gap(O[nt]);
+          }
+        }
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
@@ -883,23 +901,35 @@ BCFFT_STAMPS_SETTER(dm)
 
 namespace bcfft {
 bool dm_eligible(int n_in, int b) { return b == 128 && n_in == 32; }
+// the precise engine's forms (launch_forward_dm): fp32 outputs; a 16-bit bias with fp32 x only
+bool dftp_serves(int xdt, bool yf32, int bias_dt) {
+  return yf32 && (bias_dt == BCFFT_NONE || bias_dt == BCFFT_F32 || xdt == BCFFT_F32);
+}
 
 // mode 0: dft; 1 (exact): Y as hi + lo (BCFFT_ALGO_DFTX), which fp16 outputs always take; 2: the
-// precise engine (BCFFT_ALGO_DFTP) for fp32 x and outputs (no bias or an fp32 one). 16-bit outputs,
-// 16-bit biases, and 16-bit x (whose
-// output the reference rounds to x's dtype before the bias, :266-271), run DFTX, whose error
-// already sits far below that rounding. (The 16-bit-x instantiation of the stage-1 residual also
-// computed wrong values for the second-processed half on gfx950: DESIGN.md section 6b.)
+// precise engine (BCFFT_ALGO_DFTP) for fp32 outputs: fp32 x with no, an fp32 or a 16-bit bias, and
+// 16-bit x with no or an fp32 bias (the reference rounds 16-bit x's output to x's dtype before the
+// bias, :266-271; the kernel does the same). 16-bit outputs run DFTX, whose error already sits far
+// below their rounding. (Round 6: the 16-bit-x and 16-bit-bias instantiations had computed wrong
+// values because the residual MFMAs accumulated into the fp16 MFMAs' accumulators, an SrcC chain
+// across opcodes that gfx950 does not forward: DESIGN.md section 6b.)
 bool launch_forward_dm(int b, int n_in, int xdt, bool yf32, int mode, const void* x, int64_t n, int n_out,
                        const void* spec, const void* bias, int bias_dt, void* y, hipStream_t s) {
   if (!dm_eligible(n_in, b)) return false;
   const bool exact = mode >= 1;
-  // (a 16-bit bias on fp32 x runs DFTX too: the precise engine's BM = 2 instantiation computed
-  // wrong outputs on gfx950)
-  if (mode == 2 && yf32 && xdt == BCFFT_F32 && (bias_dt == BCFFT_NONE || bias_dt == BCFFT_F32)) {
+  if (mode == 2 && dftp_serves(xdt, yf32, bias_dt)) {
     constexpr int P = 7;                            // all three residual terms
-    if (bias_dt == BCFFT_NONE) launch_dm<BCFFT_F32, true, true, false, P, 0>(x, n, n_out, spec, bias, bias_dt, y, s);
-    else launch_dm<BCFFT_F32, true, true, false, P, 1>(x, n, n_out, spec, bias, bias_dt, y, s);
+    if (xdt == BCFFT_F32) {
+      if (bias_dt == BCFFT_NONE) launch_dm<BCFFT_F32, true, true, false, P, 0>(x, n, n_out, spec, bias, bias_dt, y, s);
+      else if (bias_dt == BCFFT_F32) launch_dm<BCFFT_F32, true, true, false, P, 1>(x, n, n_out, spec, bias, bias_dt, y, s);
+      else launch_dm<BCFFT_F32, true, true, false, P, 2>(x, n, n_out, spec, bias, bias_dt, y, s);
+    } else if (xdt == BCFFT_BF16) {
+      if (bias_dt == BCFFT_NONE) launch_dm<BCFFT_BF16, true, true, false, P, 0>(x, n, n_out, spec, bias, bias_dt, y, s);
+      else launch_dm<BCFFT_BF16, true, true, false, P, 1>(x, n, n_out, spec, bias, bias_dt, y, s);
+    } else {
+      if (bias_dt == BCFFT_NONE) launch_dm<BCFFT_F16, true, true, false, P, 0>(x, n, n_out, spec, bias, bias_dt, y, s);
+      else launch_dm<BCFFT_F16, true, true, false, P, 1>(x, n, n_out, spec, bias, bias_dt, y, s);
+    }
     return true;
   }
   // fp32 outputs with a bias add it at the store phase (BM = 1 / 2: one buffer load per 4 values);

@@ -927,9 +927,9 @@ static int forward_plan(int64_t n_tokens, int in_features, int out_features, int
   if ((algo == BCFFT_ALGO_DFTX || algo == BCFFT_ALGO_DFTP) && !dm) return -1;
   if (algo == BCFFT_ALGO_DFT && !dm && !dm64 && !dmk && !dm256 && !dm64k) return -1;
   int a = resolve_algo(algo, n_in, block_size, x_dtype, yf32, n_tokens, n_out);
-  // the precise engine serves fp32 x with fp32 outputs only; launch_forward_dm runs DFTX for 16-bit x
-  // or outputs (and for a 16-bit bias on fp32 x, which this query does not see: bcfft.h)
-  if (a == BCFFT_ALGO_DFTP && !(x_dtype == BCFFT_F32 && yf32)) a = BCFFT_ALGO_DFTX;
+  // the precise engine serves fp32 outputs (launch_forward_dm runs DFTX for 16-bit outputs, and for
+  // a 16-bit bias on 16-bit x, which this query does not see: bcfft.h)
+  if (a == BCFFT_ALGO_DFTP && !bcfft::dftp_serves(x_dtype, yf32, BCFFT_NONE)) a = BCFFT_ALGO_DFTX;
   if (a == BCFFT_ALGO_SHORT) *kernel = "bc_forward_sn_kernel";
   else if (a == BCFFT_ALGO_DFT && dmk) *kernel = "bc_forward_dmk_kernel";
   else if (a == BCFFT_ALGO_DFT && dm256) *kernel = bcfft::dm256_kernel_name(n_tokens, n_in, n_out);
