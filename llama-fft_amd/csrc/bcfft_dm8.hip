@@ -78,6 +78,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
   const int gstride = gm.stride;
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(lds));
   ANALYSIS_INIT;
+  STAMP(62);                                        // kernel entry (stamps builds: the prologue's length)
 
   // ---- x of token `wave` of M-tile m -> its slot by LDS-DMA (the buffer range zero-fills
   // tokens past n_tokens); piece q = rows 4q + (lane >> 4), 256 B each, with the slot's unit

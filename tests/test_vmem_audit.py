@@ -55,3 +55,24 @@ def test_audit_catches_round5_late_dma_variant(tmp_path):
     _, t_loop, _ = V.check(ks[name])
     assert len(t_loop) > 0
     assert any(u.op.startswith("v_mov") for _, u, *_ in t_loop)
+
+
+def test_audit_reports_a_load_whose_registers_were_renamed():
+    """Round 6: a variant that loaded the stationary fragments by asm in the prologue and waited for
+    them inside the loop got its registers moved by hipcc between the two (the wait named other
+    registers than the loads wrote). The audit once counted such touches as orphans (no wait names
+    the load); every touch of an unnamed in-flight load is a hazard now. Synthetic listing."""
+    import vmem_audit as V
+    lines = [
+        "\t;;#ASMSTART",
+        "\tbuffer_load_dwordx4 v[0:3], v8, s[4:7], 0 offen",
+        "\t;;#ASMEND",
+        "\tv_mov_b64_e32 v[4:5], v[0:1]",        # the compiler's copy of the in-flight registers
+        "\tv_mov_b64_e32 v[6:7], v[2:3]",
+        "\t;;#ASMSTART",
+        "\ts_waitcnt vmcnt(0) ; bcfft-wait v[4:7]",
+        "\t;;#ASMEND",
+        "\ts_endpgm",
+    ]
+    t_fwd, t_loop, _ = V.check(lines)
+    assert len(t_fwd) >= 2

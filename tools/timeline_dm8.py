@@ -39,6 +39,10 @@ def main():
     t0 = st[:, :, 0].min(1)
     print(f"N={n}: {st.shape[0]} workgroups stamped; start->end median {np.median(st[:, :, 63].max(1) - t0):.0f} "
           f"ticks; start spread {np.ptp(t0)}")
+    if (st[:, :, 62] != 0).all():                   # slot 62: kernel entry, before the prologue
+        pro = st[:, :, 0].min(1) - st[:, :, 62].min(1)
+        print(f"prologue (entry -> loop start, x + table + weights): median {np.median(pro):.0f} ticks, "
+              f"max {pro.max()}; entry spread over workgroups {np.ptp(st[:, :, 62].min(1))}")
     for it in range(9):
         base = 1 + 6 * it
         if not (st[:, :, base] != 0).all():

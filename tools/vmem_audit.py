@@ -342,7 +342,10 @@ def audit(lines, forward=False):
             ov = ld.dest & (ins.touch - ins.dest if ins.is_load else ins.touch)
             if not ov:
                 continue
-            if ins.idx in back:
+            if ins.idx in back or not cons:
+                # no wait names this load's registers at all: the compiler renamed them between the
+                # load and the wait meant for it (a copy / move of the in-flight registers), so every
+                # touch is a hazard (round 6: a dm8 variant with prologue-loaded fragments did this)
                 hazards.append((ld, ins, c, sorted(ov), "touched in flight"))
             else:
                 orphans += 1
