@@ -115,9 +115,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
       *reinterpret_cast<uint4*>(lds + F_OFF + 256 * t + 16 * (ch ^ fsw(t))) = tab[c];
     }
   }
-  // the group's inverse weight scales 1 / s_o (per output block) -> LDS, ahead of the weight loads
-  // (a wait for a load issued after them would hold them back)
-  if (tid < 32) reinterpret_cast<float*>(lds + OS_OFF)[tid] = osc[grp_o * 32 + tid];
   f16x8 creg[BW][KS][NT];
   {
     const uint4* img = reinterpret_cast<const uint4*>(stat + 4) + ((int64_t)(grp_o * NW + wave) * NPIECE) * 64 + lane;
@@ -128,9 +125,18 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
           creg[fb][ks][nt] = __builtin_bit_cast(f16x8, img[((fb * KS + ks) * NT + nt) * 64]);
+    // pin the loads here (hipcc would otherwise sink them into the tile loop)
+#pragma unroll
+    for (int fb = 0; fb < BW; ++fb)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(creg[fb][ks][nt]));
   }
-  lds_barrier();                                    // the table and the scales (the x DMA, older than the
-                                                    // table loads, has landed with them)
+  // the group's inverse weight scales 1 / s_o (per output block) -> LDS (after the weight loads: its wait must not hold them back)
+  if (tid < 32) reinterpret_cast<float*>(lds + OS_OFF)[tid] = osc[grp_o * 32 + tid];
+  wait_vmcnt<0>();
+  lds_barrier();
 
   // ---- stage 1 (wave w, token slot w): x rows -> X units (one fp16 term), in place, per half.
   // xwait: this wave's x DMA of the token is in flight (pieces 0-3 = half 0, behind its older y
@@ -443,18 +449,6 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
   //       m - gstride from R' (stores issued); LDS-DMA of x(m + gstride, token w) into that
   //       slot of R' (its staging reads have completed)                               | Ba |
   //   P2  stage 2 of tile m in R                                                       | Bb |
-  // LATE_W (bcfft_dm.hip's): the first tile's stage 1 runs here, with the 256 KiB of B fragments
-  // per workgroup still in flight (the prologue was ~16 % of a launch with them waited for first,
-  // profiles/r06l_timeline_dm8_prologue.txt); the tie right behind it is their first use, so the
-  // compiler's wait for them lands there, before any x DMA or y store of the loop is in flight.
-  // The loop skips iteration 0's stage 1.
-  if (wg_in_grp < n_mtiles) stage1(lds, 0, wave, false, std::integral_constant<int, 0>{});
-#pragma unroll
-  for (int fb = 0; fb < BW; ++fb)
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(creg[fb][ks][nt]));
   int64_t m = wg_in_grp;
   STAMP(0);
   for (int it = 0; m < n_mtiles || it > 0; ++it, m += gstride) {
@@ -479,7 +473,7 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm8_kernel(
         stage1(region, par, wave, true, std::integral_constant<int, GLU ? 4 : 8>{});          // stores
       }
     } else {
-      if (have && it > 0) {                         // (iteration 0's stage 1 ran before the loop)
+      if (have) {
         STAMP(sb + 1);
         // YPRIO: the transform-first waves (the younger of each SIMD pair) issue ahead of their
         // partner's stage 3: their stage 1 was the tile's critical path (6.1 k cycles against 2.6 k,
