@@ -6,7 +6,8 @@ table, 2: the weight spectra, 3: the stage-3 table; dm_model precise=True, terms
   * the north star's random operator (seed 0), 64 tokens (Frobenius; the reference's T5 bar 1e-4);
   * the weight residual in other formats than e4m3 (exact, and MX-style e2m1 / e2m3 / e3m2 with a
     power-of-two scale per 16 or 4 input blocks), to see how few bits the residual may take.
-usage: python tools/precision_terms.py   (writes nothing; profiles/r05_precision_terms.txt holds a run)"""
+usage: python tools/precision_terms.py   (writes nothing; profiles/r06q_precision_terms_narrow_residual.txt
+holds a run)"""
 import os
 import sys
 
@@ -70,6 +71,11 @@ def mx_quant(r, i, mant, maxv, grp=16):
     return q(R).reshape(no, ni, h), q(I).reshape(no, ni, h)
 
 
+# (name, mantissa bits, largest value, input blocks per power-of-two scale)
+NARROW = (("e2m1, scale per 16 blocks", 1, 6.0, 16), ("e2m1, scale per 4 blocks", 1, 6.0, 4),
+          ("e2m3, scale per 16 blocks", 3, 7.5, 16), ("e3m2, scale per 16 blocks", 2, 28.0, 16))
+
+
 def report(name, x, c, ref, **kw):
     y = DM.dm_forward(x, c, **kw)
     d = (y - ref).astype(np.float64)
@@ -93,8 +99,7 @@ def main():
     try:
         DM.lo8_image = lambda cc: tuple(raw_residual(cc))
         report("weight residual exact", xs, c, rs, precise=True)
-        for name, mant, maxv, grp in (("e2m1, scale per 16 blocks", 1, 6.0, 16), ("e2m1, scale per 4 blocks", 1, 6.0, 4),
-                                      ("e2m3, scale per 16 blocks", 3, 7.5, 16), ("e3m2, scale per 16 blocks", 2, 28.0, 16)):
+        for name, mant, maxv, grp in NARROW:
             DM.lo8_image = lambda cc, m=mant, v=maxv, g=grp: mx_quant(*raw_residual(cc), m, v, g)
             report(f"weight residual {name}", xs, c, rs, precise=True)
     finally:
@@ -109,6 +114,13 @@ def main():
     report("dftx", x, c, ref, exact=True)
     for t in [(1, 0, 0), (0, 1, 0), (0, 0, 1), (1, 1, 0), (1, 0, 1), (0, 1, 1), (1, 1, 1)]:
         report(f"precise, residual terms {t}", x, c, ref, precise=True, terms=t)
+    print("north-star operator (random, seed 0), 64 tokens: narrow weight residuals", flush=True)
+    try:
+        for name, mant, maxv, grp in NARROW:
+            DM.lo8_image = lambda cc, m=mant, v=maxv, g=grp: mx_quant(*raw_residual(cc), m, v, g)
+            report(f"weight residual {name}", x, c, ref, precise=True)
+    finally:
+        DM.lo8_image = orig
 
 
 if __name__ == "__main__":
