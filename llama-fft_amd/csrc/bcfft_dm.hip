@@ -136,9 +136,10 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
   // half the waves would idle through them: the first stage 1 runs one half of each token on its
   // F wave and the other on its I wave (fp32 x: the halves are in place independently; the
   // prologue's x DMA is split the same way), and the last stage 3 one N-tile on each
-  // (not in the precise engine: its residual operands leave no registers for the split paths)
+  // (the precise engine: the drain split only, and not with an fp32 bias; its residual operands
+  // leave no registers for the fill split, and those two spill 20 B per lane: DESIGN.md section 8b)
   constexpr bool FILL_SPLIT = LATE_W && ES == 4 && EP == 0;
-  constexpr bool DRAIN_SPLIT = !GLU && EP == 0;
+  constexpr bool DRAIN_SPLIT = !GLU && (EP == 0 || BM != 1);
   // (round 4 measured and rejected other x-DMA placements and role splits: docs/HISTORY.md section 8c,
   // item 8, with their A/B logs; their switches are in the git history of this file)
 
