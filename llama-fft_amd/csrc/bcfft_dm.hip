@@ -864,9 +864,15 @@ __global__ __launch_bounds__(512, 2) void bc_forward_dm_kernel(
     STAMP(sb + 2);
     // F wave j streams the next tile's x for its slot j of the other region in one burst: stage 3
     // has read that slot's Y and staged y (each wave's LDS reads completed before Ba)
-    if (fwave && m + gstride < n_mtiles && !(EARLY_X && it == 0)) dma_token(m + gstride, other, 0, NDMA);
+    // (EP: after stage 2 instead. Loads return in order, so a wait for a lo8 refill issued behind
+    // the DMA waits for the DMA too: DESIGN.md section 6c)
+    const bool dma_now = fwave && m + gstride < n_mtiles && !(EARLY_X && it == 0);
+    if (dma_now && (EP & 2) == 0) dma_token(m + gstride, other, 0, NDMA);
     STAMP(sb + 3);
     stage2(region, par, clr);
+    if constexpr ((EP & 2) != 0) {
+      if (dma_now) dma_token(m + gstride, other, 0, NDMA);
+    }
     if (EARLY_X && it == 0 && !fwave) wait_vmcnt<0>();   // the next tile's x (issued by this I wave) has landed
     STAMP(sb + 4);
     lds_barrier();                                  // Bb: Y units complete
